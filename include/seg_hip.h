@@ -1,0 +1,123 @@
+/* seg_hip.h — C ABI of libseg_hip.so, the MI355X (gfx950) training path for the
+ * hierarchical weak-label segmentation model of pmeletis/IV2019-boosting-semantic-
+ * segmentation-with-weak-labels.
+ *
+ * The reference exposes this path through Python/TF plugin functions; each entry point
+ * below replaces the TF graph that one of them builds (paths relative to the reference's
+ * code/ directory):
+ *
+ *   seg_create / seg_destroy      model(...) graph construction + variable creation
+ *                                 (models/resnet50_extended_model_hierarchical.py:17-141,
+ *                                  models/resnet50_extended_feature_extractor.py:8-51)
+ *   seg_forward                   the TRAIN-mode forward pass of model(...) up to the
+ *                                 low-resolution logits (hierarchical.py:102-134)
+ *   seg_loss                      upsampler + softmax/argmax/decision fusion
+ *                                 (hierarchical.py:135-168) and define_losses(TRAIN)
+ *                                 (estimator/define_losses_hierarchical.py:14-217)
+ *   seg_backward                  tf.gradients inside create_train_op
+ *                                 (estimator/define_estimator_hierarchical.py:120-129)
+ *   seg_apply_update              MomentumOptimizer.apply_gradients + UPDATE_OPS (BN moving
+ *                                 averages, EMA) (estimator/define_optimizer.py:3-26,
+ *                                 define_estimator_hierarchical.py:96-111)
+ *   seg_confusion                 define_metrics.mean_iou's confusion matrix
+ *                                 (estimator/define_metrics.py:5-20)
+ *
+ * Conventions: every function returns 0 on success or a negative errno-style code;
+ * seg_last_error() describes the failure. Device buffers passed in are caller-owned; the
+ * context owns activations and workspace. NHWC layout. Every launch goes to the explicit
+ * stream argument; no call allocates, frees or synchronises inside a step, so a step can
+ * be captured in a hipGraph. One context per device; not re-entrant per context.
+ */
+#ifndef SEG_HIP_H
+#define SEG_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct seg_ctx seg_ctx;
+
+enum { SEG_PYRAMID_NONE = 0, SEG_PYRAMID_PSP = 1, SEG_PYRAMID_ASPP = 2 };
+enum { SEG_DTYPE_F32 = 0, SEG_DTYPE_BF16 = 1 };
+enum { SEG_DATASET_CITYSCAPES = 0, SEG_DATASET_VISTAS = 1 };
+enum { SEG_PARAM_WEIGHTS = 0, SEG_PARAM_GAMMA = 1, SEG_PARAM_BETA = 2,
+       SEG_PARAM_MOVING_MEAN = 3, SEG_PARAM_MOVING_VAR = 4 };
+
+typedef struct seg_cfg {
+  int depth;            /* 50 | 101 (name_feature_extractor) */
+  int pyramid;          /* SEG_PYRAMID_* (psp_module; ASPP is the commented spec) */
+  int height, width;    /* height/width_feature_extractor */
+  int nb_pp, nb_pb, nb_pi;  /* per-GPU per-pixel / per-bbox / per-image sub-batches */
+  int dtype;            /* SEG_DTYPE_*: compute/storage dtype (accumulation is fp32) */
+  int dataset;          /* SEG_DATASET_* (per_pixel_dataset_name) */
+  int output_stride;    /* stride_feature_extractor (8) */
+  int feature_dims;     /* feature_dims_decreased (256) */
+  float bn_decay;       /* batch_norm_decay (0.9) */
+  int train_bn;         /* norm_train_variables */
+  float weight_decay;   /* regularization_weight (0.00017): l2_regularizer scale */
+} seg_cfg;
+
+/* lifecycle -------------------------------------------------------------------------- */
+int seg_create(int device, const seg_cfg* cfg, seg_ctx** out);
+int seg_destroy(seg_ctx* ctx);
+const char* seg_last_error(seg_ctx* ctx);   /* ctx may be NULL (creation errors) */
+
+/* parameters: flat fp32 buffers, allocated by the caller (sizes from seg_sizes) --------
+ * params  [n_train]            conv weights ([Co][KH][KW][Ci]) then BN gamma/beta
+ * grads   [n_train + n_stats]  gradient of the segmentation loss; the tail holds this
+ *                              step's BN batch statistics (mean, Bessel variance) so one
+ *                              all-reduce averages both across data-parallel ranks
+ * momentum[n_train], ema[n_train] (optional, may be NULL), moving[n_moving] */
+int seg_sizes(seg_ctx* ctx, int64_t* n_train, int64_t* n_decay, int64_t* n_moving,
+              int64_t* n_stats);
+int seg_bind_buffers(seg_ctx* ctx, float* params, float* grads, float* momentum, float* ema,
+                     float* moving);
+int64_t seg_param_count(seg_ctx* ctx);
+int seg_param_info(seg_ctx* ctx, int64_t i, const char** name, int64_t* offset,
+                   int64_t* numel, int* kind);
+/* dims[4]: weights (Co, KH, KW, Ci); BN vectors (C, 1, 1, 1) */
+int seg_param_shape(seg_ctx* ctx, int64_t i, int64_t* dims);
+/* re-derive compute copies (bf16 weights, flipped dgrad weights) after a host write */
+int seg_params_updated(seg_ctx* ctx, void* stream);
+
+/* one training step -------------------------------------------------------------------- */
+int seg_forward(seg_ctx* ctx, const float* images_nhwc, void* stream);
+int seg_loss(seg_ctx* ctx, const int32_t* px_labels, const float* bbox_soft,
+             const float* tag_soft, int32_t* decisions_out, void* stream);
+int seg_backward(seg_ctx* ctx, void* stream);
+/* lr, momentum; ema_decay_eff = min(ema_decay, (1+step)/(10+step)) or 0 to skip EMA;
+ * grad_scale multiplies the gradient (1/world_size after a SUM all-reduce) */
+int seg_apply_update(seg_ctx* ctx, float lr, float momentum, float ema_decay_eff,
+                     float grad_scale, void* stream);
+
+/* outputs ------------------------------------------------------------------------------
+ * losses: device float[10] = {segmentation, l1, l2_vehicle, l2_human, n1, n2v, n2h,
+ *         f1, f2v, f2h}; reg: device float[1] regularisation value of the last update
+ *         (weights before the update) */
+int seg_outputs(seg_ctx* ctx, const float** losses, const float** reg,
+                const float** logits_lowres, int* ld_logits, int* h_low, int* w_low);
+int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions, int64_t n,
+                  int num_classes, int32_t* cm, void* stream);
+
+/* kernel-time profiling of conv classes (0 fwd, 1 dgrad, 2 wgrad) ---------------------- */
+int seg_profile(seg_ctx* ctx, int enable);
+int seg_profile_read(seg_ctx* ctx, int cls, double* ms_total, double* gflop_total,
+                     int64_t* launches, double* ms_max_layer, char* layer_name, int name_len);
+
+/* single-op entry points (parity tests of individual kernels) -------------------------- */
+int seg_op_conv_fwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+                    const void* w, int Co, int k, int stride, int rate, int explicit_pad,
+                    void* y, int ldy, float* stats, void* stream);
+int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
+                      const void* w, int Ci, int k, int stride, int rate, int explicit_pad,
+                      int H, int W, void* dx, int lddx, void* stream);
+int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
+                      const void* x, int H, int W, int Ci, int ldx, int k, int stride, int rate,
+                      int explicit_pad, float* dw, void* workspace, int64_t ws_bytes,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

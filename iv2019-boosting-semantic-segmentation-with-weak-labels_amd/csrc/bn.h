@@ -1,0 +1,57 @@
+// Batch normalisation (TF 1.12 fused training semantics) as HBM-streaming kernels.
+//   forward : per-channel (mean, biased var) from the conv epilogue's tile partials
+//             (Chan merge, fixed order), out = act((y-mean)*gamma*rsqrt(var+eps) + beta [+res])
+//   backward: dyhat = dz * [z>0]; dgamma = sum dyhat*xhat; dbeta = sum dyhat;
+//             dy = gamma*invstd*(dyhat - mean(dyhat) - xhat*mean(dyhat*xhat))
+#pragma once
+#include "seg_common.h"
+
+#define SEG_BN_EPS 1.001e-5f  // tf.nn.fused_batch_norm clamps 1e-5 up to this
+
+struct BnState {     // per-layer per-step device vectors, each [C]
+  float* mean;
+  float* invstd;
+  float* scale;      // gamma * invstd
+  float* var_unb;    // Bessel-corrected batch variance (moving-average input)
+  float* sdy;        // backward: mean(dyhat)
+  float* sdyx;       // backward: mean(dyhat * xhat)
+};
+
+struct BnApplyArgs {
+  const void* y; int ldy;          // conv output (T)
+  long M; int C;
+  const float* mean; const float* scale; const float* beta;
+  int relu;
+  // residual 1: plain tensor (T) with optional spatial subsampling (stride rs over an
+  // [N][Hr][Wr] grid; the output grid is [N][Ho][Wo])
+  const void* res; int ldres; int rs; int Ho, Wo, Hr, Wr;
+  // residual 2: second BN (shortcut conv): (y2-mean2)*scale2+beta2
+  const void* y2; int ldy2; const float* mean2; const float* scale2; const float* beta2;
+  void* out; int ldo;              // output (T or f32)
+};
+
+struct BnBwdArgs {
+  const void* dz; int lddz;        // incoming gradient (T or f32)
+  const void* z; int ldz;          // activation whose >0 mask gates dz (nullable)
+  const void* y; int ldy;          // conv output (T)
+  long M; int C;
+  const float* mean; const float* invstd; const float* scale;
+  const float* sdy; const float* sdyx;   // apply: means from finalize
+  void* dy; int lddy;              // output gradient wrt y (T)
+  void* dyhat; int lddyhat;        // optional masked gradient (T)
+  const float* dzscale;            // optional per-channel factor applied to dz
+  float* part;                     // reduce partials [rb][C][2]
+  int rb;                          // number of row blocks
+};
+
+hipError_t launch_bn_stats_finalize(const float* tile_part, long M, int C, int tile_rows,
+                                    float* scratch, const float* gamma, BnState st,
+                                    hipStream_t s);
+hipError_t launch_bn_apply(int dtype, int out_f32, const BnApplyArgs& a, hipStream_t s);
+int bn_bwd_rowblocks(long M, int C);
+hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipStream_t s);
+hipError_t launch_bn_bwd_finalize(const float* part, int rb, long M, int C, BnState st,
+                                  float* dgamma, float* dbeta, hipStream_t s);
+hipError_t launch_bn_bwd_apply(int dtype, int dz_f32, const BnBwdArgs& a, hipStream_t s);
+hipError_t launch_moving_update(float* mov_mean, float* mov_var, const float* bmean,
+                                const float* bvar, int n, float decay, hipStream_t s);

@@ -1,0 +1,49 @@
+// Implicit-GEMM convolutions on CDNA4 MFMA (gfx950). No im2col buffer is ever built: the
+// A-operand gather computes each source pixel (with TF padding / dilation / stride) while
+// staging tiles into LDS.
+//
+//   forward : y[p][co]  = sum_{kh,kw,ci} x[src(p,kh,kw)][ci] * w[co][kh][kw][ci]
+//   dgrad   : dx[p][ci] = sum_{kh,kw,co} dy[src_t(p,kh,kw)][co] * wT[ci][kh][kw][co]
+//             (wT = spatially flipped, transposed weights; stride>1 uses the divisibility
+//              gather of a transposed conv)
+//   wgrad   : dw[co][kh][kw][ci] = sum_p dy[p][co] * x[src(p,kh,kw)][ci]   (split-K slabs)
+#pragma once
+#include "seg_common.h"
+
+struct ConvArgs {
+  const void* x;  // A source, NHWC [N][H][W][ldx]
+  int N, H, W, C, ldx;
+  const void* w;  // B, [Co][K] with row stride ldw (K = KH*KW*C)
+  int ldw;
+  void* y;        // output NHWC [N][Ho][Wo][ldy]
+  int Ho, Wo, Co, ldy;
+  const void* r;  // optional residual added in the epilogue (may alias y), ld = ldr
+  int ldr;
+  const void* r2; // optional second residual, ld = ldr2
+  int ldr2;
+  int KH, KW;
+  int sf;         // forward stride: src = o*sf - pad + k*dil
+  int st;         // transposed stride: src valid iff divisible by st (1 = plain conv)
+  int pad_h, pad_w, dil;
+  float* stats;   // BN partials [mtiles][Co] x {sum, M2} (nullptr = none)
+};
+
+struct WgradArgs {
+  const void* dy;  // [P][lddy], P = N*Ho*Wo
+  int lddy;
+  const void* x;   // NHWC [N][H][W][ldx]
+  int N, H, W, C, ldx;
+  int Ho, Wo, Co;
+  int KH, KW, sf, pad_h, pad_w, dil;
+  float* out;      // fp32 [splits][Co][KH*KW*C]
+  int splits;
+};
+
+// host launchers (conv.hip); return hipError_t
+hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t s);
+hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s);
+hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride, long n,
+                                float* out, int accumulate, hipStream_t s);
+hipError_t launch_weight_flip_transpose(int dtype, const void* w, void* wt, int co, int kh, int kw,
+                                        int ci, hipStream_t s);
+int conv_nt_mtiles(long M);  // rows per BN-stat partial = 128

@@ -1,0 +1,1128 @@
+// Native runtime of the training step: builds the dilated-ResNet + pyramid + hierarchical
+// heads graph (slim resnet_v1 unit schedule, reference models/*), owns activations and
+// workspace, sequences the HIP kernels for forward / loss / backward / update, and exports
+// the C ABI declared in include/seg_hip.h.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/seg_hip.h"
+#include "bn.h"
+#include "conv.h"
+#include "loss.h"
+#include "optim.h"
+#include "pool.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(std::string* dst, int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (dst) *dst = buf;
+  g_err = buf;
+  return code;
+}
+
+struct Act {
+  void* p = nullptr;
+  int N = 0, H = 0, W = 0, C = 0, ld = 0;
+  long M() const { return (long)N * H * W; }
+};
+
+struct ConvL {
+  std::string name;
+  int ci, co, k, stride, rate;
+  bool explicit_pad, relu;
+  long w_off = 0, g_off = 0, b_off = 0, mv_off = 0;  // flat offsets
+  int N = 0, H = 0, W = 0, Ho = 0, Wo = 0, pad_h = 0, pad_w = 0;
+  int co_pad = 0;                 // wgrad row padding (co % 8 != 0)
+  void* w_lp = nullptr;           // compute-dtype weights [co][k][k][ci]
+  void* wt_lp = nullptr;          // flipped transpose [ci][k][k][co] (dgrad)
+  bool need_dgrad = true;
+  Act y, dy;                      // conv output and its gradient
+  BnState st{};
+  float* stats_part = nullptr;    // [mtiles][co][2]
+  float* bwd_part = nullptr;      // [rb][co][2]
+  int rb = 1;
+};
+
+enum ShortcutKind { SC_IDENTITY = 0, SC_SUBSAMPLE = 1, SC_CONV = 2 };
+
+struct Unit {
+  int sc = -1, c1 = -1, c2 = -1, c3 = -1;
+  ShortcutKind kind = SC_IDENTITY;
+  int stride = 1;
+  Act in, out;        // in is not owned (previous output)
+  Act z1, z2;         // post BN+ReLU of conv1/conv2
+  Act dz1, dz2, dpre; // gradients; dpre = relu-masked gradient of out (identity/subsample)
+  Act dout;           // gradient wrt out (owned)
+};
+
+struct Prof {
+  bool on = false;
+  std::vector<hipEvent_t> ev;
+  struct Rec { int cls; int layer; double gflop; int e0, e1; };
+  std::vector<Rec> recs;
+  int next = 0;
+};
+
+}  // namespace
+
+struct seg_ctx {
+  seg_cfg cfg{};
+  int device = 0;
+  int dt = SEG_BF16;
+  size_t esz = 2;
+  std::string err;
+  std::vector<void*> allocs;
+
+  // parameters
+  std::vector<ConvL> convs;
+  long n_train = 0, n_decay = 0, n_moving = 0, n_stats = 0;
+  struct PInfo { std::string name; long off, numel; int kind; int dims[4]; };
+  std::vector<PInfo> pinfo;
+  float* params = nullptr;
+  float* grads = nullptr;
+  float* mom = nullptr;
+  float* ema = nullptr;
+  float* moving = nullptr;
+  void* w_lp_flat = nullptr;      // bf16 copy of the conv-weight region (bf16 mode)
+
+  // graph
+  Act img;                        // compute-dtype images
+  int stem = -1;
+  Act z0, dz0, p0, dp0;
+  int pool_ph = 0, pool_pw = 0;
+  std::vector<Unit> units;
+  int dfd = -1;
+  Act z_dfd, dz_dfd;              // z_dfd may be a slice of concat
+  // pyramid
+  std::vector<int> pyr_conv;      // per branch conv index
+  std::vector<int> pyr_k;         // grid size per branch
+  std::vector<Act> pooled, dpooled, zb, dzb;
+  int pyr_final = -1;
+  Act concat, dconcat;
+  Act feat, dfeat;
+  GridSpec pool_grids{};          // avg-pool grids over z_dfd
+  std::vector<GridSpec> up_grids; // resize-transpose per branch
+  float* grid_part = nullptr;     // [N][Hf][cells][C]
+  // heads
+  Unit heads[3];
+  int logit_conv[3] = {-1, -1, -1};
+  Act logits;                     // fp32 [N][Hl][Wl][ldl]
+  float* grad_un = nullptr;       // fp32 same shape
+  int ldl = 0, nc[3] = {0, 0, 0};
+  LossTables tables{};
+  float* loss_part = nullptr;
+  int loss_blocks = 0;
+  float* loss_out = nullptr;      // [10]
+  float* dzscale = nullptr;       // [ldl]
+  float* reg_part = nullptr;
+  float* reg_out = nullptr;
+  // workspace
+  float* slab = nullptr;
+  size_t slab_floats = 0;
+  float* stat_scratch = nullptr;
+  size_t stat_scratch_floats = 0;
+  Prof prof;
+  bool bound = false;
+};
+
+namespace {
+
+int hip_fail(seg_ctx* c, hipError_t e, const char* where) {
+  return set_err(c ? &c->err : nullptr, -EIO, "%s: %s", where, hipGetErrorString(e));
+}
+#define HIPCALL(c, expr)                                    \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
+    if (_e != hipSuccess) return hip_fail((c), _e, #expr);  \
+  } while (0)
+
+template <typename T>
+int dalloc(seg_ctx* c, T** p, size_t count) {
+  void* q = nullptr;
+  size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  hipError_t e = hipMalloc(&q, bytes);
+  if (e != hipSuccess) return hip_fail(c, e, "hipMalloc");
+  (void)hipMemset(q, 0, bytes);
+  c->allocs.push_back(q);
+  *p = (T*)q;
+  return 0;
+}
+
+int alloc_act(seg_ctx* c, Act& a, int N, int H, int W, int C, int ld = 0, size_t esz = 0) {
+  a.N = N; a.H = H; a.W = W; a.C = C; a.ld = ld ? ld : C;
+  size_t e = esz ? esz : c->esz;
+  char* p = nullptr;
+  int r = dalloc(c, &p, (size_t)a.M() * a.ld * e);
+  a.p = p;
+  return r;
+}
+
+Act slice(const seg_ctx* c, const Act& a, int c_off, int C) {
+  Act v = a;
+  v.p = (char*)a.p + (size_t)c_off * c->esz;
+  v.C = C;
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// architecture (slim resnet_v1 / stack_blocks_dense; reference models/* — see oracle/tfseg)
+// ------------------------------------------------------------------------------------------
+int add_conv(seg_ctx* c, const std::string& name, int ci, int co, int k, int stride, int rate,
+             bool explicit_pad, bool relu) {
+  ConvL L;
+  L.name = name; L.ci = ci; L.co = co; L.k = k; L.stride = stride; L.rate = rate;
+  L.explicit_pad = explicit_pad; L.relu = relu;
+  c->convs.push_back(L);
+  return (int)c->convs.size() - 1;
+}
+
+struct UnitSpec { std::string scope; int din, d, dbn, s, r; };
+
+std::vector<UnitSpec> resnet_units(int depth, int output_stride) {
+  const int n3 = depth == 101 ? 23 : 6;
+  struct B { const char* n; int base, units, stride; } blocks[4] = {
+      {"block1", 64, 3, 2}, {"block2", 128, 4, 2}, {"block3", 256, n3, 2}, {"block4", 512, 3, 1}};
+  const int target = output_stride / 4;
+  int current = 1, rate = 1, din = 64;
+  std::vector<UnitSpec> out;
+  for (auto& b : blocks) {
+    for (int i = 0; i < b.units; ++i) {
+      int us = i == b.units - 1 ? b.stride : 1;
+      std::string scope = std::string(b.n) + "/unit_" + std::to_string(i + 1) + "/bottleneck_v1";
+      if (current == target) {
+        out.push_back({scope, din, b.base * 4, b.base, 1, rate});
+        rate *= us;
+      } else {
+        out.push_back({scope, din, b.base * 4, b.base, us, 1});
+        current *= us;
+      }
+      din = b.base * 4;
+    }
+  }
+  return out;
+}
+
+void add_bottleneck(seg_ctx* c, Unit& u, const std::string& scope, int din, int d, int dbn, int s,
+                    int r) {
+  if (d != din) {
+    u.sc = add_conv(c, scope + "/shortcut", din, d, 1, s, 1, false, false);
+    u.kind = SC_CONV;
+  } else {
+    u.kind = s > 1 ? SC_SUBSAMPLE : SC_IDENTITY;
+  }
+  u.stride = s;
+  u.c1 = add_conv(c, scope + "/conv1", din, dbn, 1, 1, 1, false, true);
+  u.c2 = add_conv(c, scope + "/conv2", dbn, dbn, 3, s, r, s > 1, true);
+  u.c3 = add_conv(c, scope + "/conv3", dbn, d, 1, 1, 1, false, false);
+}
+
+void fill_tables(LossTables& t, int dataset) {
+  memset(&t, 0, sizeof(t));
+  if (dataset == SEG_DATASET_VISTAS) {
+    // define_losses_hierarchical.py:37-74; hierarchical.py:146-156
+    t.c1 = 53; t.c2 = 12; t.c3 = 5; t.n_pp = 66; t.n_pb = 15;
+    t.cid_l1_vehicle = 49; t.cid_l1_human = 19; t.l1_wmax = 51;
+    const int pp2l1[66] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19,
+                           19, 19, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34,
+                           35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 49, 49, 49,
+                           49, 49, 49, 49, 49, 49, 49, 50, 51, 52};
+    const int pb2l1[15] = {49, 49, 49, 49, 49, 49, 19, 19, 19, 19, 19, 52, 52, 52, 52};
+    (void)pb2l1;
+    int pp2veh[66], pp2hum[66];
+    for (int i = 0; i < 66; ++i) { pp2veh[i] = 11; pp2hum[i] = 4; }
+    for (int i = 0; i < 11; ++i) pp2veh[52 + i] = i;
+    pp2hum[19] = 0; pp2hum[20] = 1; pp2hum[21] = 2; pp2hum[22] = 3;
+    const int pb2veh[15] = {0, 2, 3, 5, 6, 9, 11, 11, 11, 11, 11, 11, 11, 11, 11};
+    const int pb2hum[15] = {4, 4, 4, 4, 4, 4, 0, 0, 0, 0, 0, 4, 4, 4, 4};
+    for (int i = 0; i < 66; ++i) { t.pp2l1[i] = pp2l1[i]; t.pp2veh[i] = pp2veh[i]; t.pp2hum[i] = pp2hum[i]; }
+    for (int i = 0; i < 15; ++i) { t.pb2veh[i] = pb2veh[i]; t.pb2hum[i] = pb2hum[i]; }
+    for (int i = 0; i < 20; ++i) t.l1_to_common[i] = i;
+    for (int i = 20; i < 50; ++i) t.l1_to_common[i] = i + 3;
+    t.l1_to_common[50] = 63; t.l1_to_common[51] = 64; t.l1_to_common[52] = 65;
+    for (int i = 0; i < 11; ++i) t.veh_to_common[i] = 52 + i;
+    t.veh_to_common[11] = 65;
+    const int h2c[5] = {19, 20, 21, 22, 65};
+    for (int i = 0; i < 5; ++i) t.hum_to_common[i] = h2c[i];
+  } else {
+    // define_losses_hierarchical.py:75-93; hierarchical.py:157-162
+    t.c1 = 14; t.c2 = 7; t.c3 = 3; t.n_pp = 20; t.n_pb = 15;
+    t.cid_l1_vehicle = 12; t.cid_l1_human = 11; t.l1_wmax = 12;
+    const int pp2l1[20] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 11, 12, 12, 12, 12, 12, 12, 13};
+    const int pp2veh[20] = {6, 6, 6, 6, 6, 6, 6, 6, 6, 6, 6, 6, 6, 0, 1, 2, 3, 4, 5, 6};
+    const int pp2hum[20] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 0, 1, 2, 2, 2, 2, 2, 2, 2};
+    const int pb2veh[15] = {5, 2, 0, 4, 3, 1, 6, 6, 6, 6, 6, 6, 6, 6, 6};
+    const int pb2hum[15] = {2, 2, 2, 2, 2, 2, 0, 0, 0, 0, 0, 2, 2, 2, 2};
+    for (int i = 0; i < 20; ++i) { t.pp2l1[i] = pp2l1[i]; t.pp2veh[i] = pp2veh[i]; t.pp2hum[i] = pp2hum[i]; }
+    for (int i = 0; i < 15; ++i) { t.pb2veh[i] = pb2veh[i]; t.pb2hum[i] = pb2hum[i]; }
+    const int l1c[14] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 19};
+    const int vc[7] = {13, 14, 15, 16, 17, 18, 19};
+    const int hc[3] = {11, 12, 19};
+    for (int i = 0; i < 14; ++i) t.l1_to_common[i] = l1c[i];
+    for (int i = 0; i < 7; ++i) t.veh_to_common[i] = vc[i];
+    for (int i = 0; i < 3; ++i) t.hum_to_common[i] = hc[i];
+  }
+}
+
+// TF ResizeBilinear(align_corners=True) legacy index/lerp (float arithmetic)
+void tf_lerp_host(int o, int n_in, int n_out, int& lo, int& hi, float& l) {
+  float scale = n_out > 1 ? (float)(n_in - 1) / (float)(n_out - 1) : 0.f;
+  float fin = (float)o * scale;
+  lo = (int)fin;
+  hi = std::min(lo + 1, n_in - 1);
+  l = fin - (float)lo;
+}
+
+// geometry of a conv on an input of spatial size (H, W)
+void conv_geom(ConvL& L, int N, int H, int W) {
+  L.N = N; L.H = H; L.W = W;
+  const int keff = L.k + (L.k - 1) * (L.rate - 1);
+  if (L.explicit_pad) {  // conv2d_same, stride > 1: pad (keff-1)//2 before, rest after, VALID
+    L.pad_h = L.pad_w = (keff - 1) / 2;
+    L.Ho = (H + keff - 1 - keff) / L.stride + 1;
+    L.Wo = (W + keff - 1 - keff) / L.stride + 1;
+  } else {               // SAME (only stride 1 here): out = ceil(n/s)
+    L.Ho = (H + L.stride - 1) / L.stride;
+    L.Wo = (W + L.stride - 1) / L.stride;
+    int tot_h = std::max((L.Ho - 1) * L.stride + keff - H, 0);
+    int tot_w = std::max((L.Wo - 1) * L.stride + keff - W, 0);
+    L.pad_h = tot_h / 2;
+    L.pad_w = tot_w / 2;
+  }
+}
+
+int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
+  conv_geom(L, N, H, W);
+  L.co_pad = (L.co % 8) ? ((L.co + 15) / 16) * 16 : L.co;
+  int ld = ldy ? ldy : L.co_pad;
+  if (int r = alloc_act(c, L.y, N, L.Ho, L.Wo, L.co, ld)) return r;
+  if (int r = alloc_act(c, L.dy, N, L.Ho, L.Wo, L.co, ld)) return r;
+  float* v;
+  if (int r = dalloc(c, &v, (size_t)6 * L.co)) return r;
+  L.st.mean = v; L.st.invstd = v + L.co; L.st.scale = v + 2 * L.co; L.st.var_unb = v + 3 * L.co;
+  L.st.sdy = v + 4 * L.co; L.st.sdyx = v + 5 * L.co;
+  long M = (long)N * L.Ho * L.Wo;
+  if (int r = dalloc(c, &L.stats_part, (size_t)conv_nt_mtiles(M) * L.co * 2)) return r;
+  L.rb = bn_bwd_rowblocks(M, L.co);
+  if (int r = dalloc(c, &L.bwd_part, (size_t)L.rb * L.co * 2)) return r;
+  size_t need = (size_t)((conv_nt_mtiles(M) + 63) / 64) * L.co * 3;
+  c->stat_scratch_floats = std::max(c->stat_scratch_floats, need);
+  return 0;
+}
+
+int wgrad_splits(const ConvL& L) {
+  const int BM = L.co_pad <= 64 ? 64 : 128;
+  const int BN = 128;
+  long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * L.ci + BN - 1) / BN);
+  long P = (long)L.N * L.Ho * L.Wo;
+  long s = std::max<long>(1, 1024 / std::max<long>(tiles, 1));
+  long maxs = std::max<long>(1, P / 2048);
+  s = std::min(s, maxs);
+  return (int)std::min<long>(s, 256);
+}
+
+// ------------------------------------------------------------------------------------------
+// kernel sequencing helpers
+// ------------------------------------------------------------------------------------------
+struct Step {
+  seg_ctx* c;
+  hipStream_t s;
+  int dt;
+};
+
+int prof_begin(seg_ctx* c, hipStream_t s, int cls, int layer, double gflop, int* slot) {
+  *slot = -1;
+  if (!c->prof.on) return 0;
+  if (c->prof.next + 2 > (int)c->prof.ev.size()) return 0;
+  int e0 = c->prof.next++, e1 = c->prof.next++;
+  HIPCALL(c, hipEventRecord(c->prof.ev[e0], s));
+  c->prof.recs.push_back({cls, layer, gflop, e0, e1});
+  *slot = (int)c->prof.recs.size() - 1;
+  return 0;
+}
+int prof_end(seg_ctx* c, hipStream_t s, int slot) {
+  if (slot < 0) return 0;
+  HIPCALL(c, hipEventRecord(c->prof.ev[c->prof.recs[slot].e1], s));
+  return 0;
+}
+
+int conv_forward(Step& S, int li, const Act& x) {
+  seg_ctx* c = S.c;
+  ConvL& L = c->convs[li];
+  ConvArgs a{};
+  a.x = x.p; a.N = x.N; a.H = x.H; a.W = x.W; a.C = x.C; a.ldx = x.ld;
+  a.w = L.w_lp; a.ldw = L.k * L.k * L.ci;
+  a.y = L.y.p; a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co; a.ldy = L.y.ld;
+  a.KH = a.KW = L.k; a.sf = L.stride; a.st = 1; a.pad_h = L.pad_h; a.pad_w = L.pad_w;
+  a.dil = L.rate; a.stats = L.stats_part;
+  long M = (long)x.N * L.Ho * L.Wo;
+  int slot;
+  if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
+  HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
+  HIPCALL(c, launch_bn_stats_finalize(L.stats_part, M, L.co, 128, c->stat_scratch,
+                                      c->params + L.g_off, L.st, S.s));
+  return 0;
+}
+
+// out = act(bn(y) [+ residual])
+int bn_apply(Step& S, int li, const Act& out, int out_f32, const Act* res = nullptr, int rs = 1,
+             int li2 = -1, int relu = -1) {
+  seg_ctx* c = S.c;
+  ConvL& L = c->convs[li];
+  BnApplyArgs a{};
+  a.y = L.y.p; a.ldy = L.y.ld; a.M = L.y.M(); a.C = L.co;
+  a.mean = L.st.mean; a.scale = L.st.scale; a.beta = c->params + L.b_off;
+  a.relu = relu < 0 ? (L.relu ? 1 : 0) : relu;
+  if (res) {
+    a.res = res->p; a.ldres = res->ld; a.rs = rs; a.Ho = L.Ho; a.Wo = L.Wo; a.Hr = res->H;
+    a.Wr = res->W;
+  }
+  if (li2 >= 0) {
+    ConvL& L2 = c->convs[li2];
+    a.y2 = L2.y.p; a.ldy2 = L2.y.ld; a.mean2 = L2.st.mean; a.scale2 = L2.st.scale;
+    a.beta2 = c->params + L2.b_off;
+  }
+  a.out = out.p; a.ldo = out.ld;
+  HIPCALL(c, launch_bn_apply(S.dt, out_f32, a, S.s));
+  return 0;
+}
+
+// BN backward for layer li: dz (gradient wrt BN output), z (mask source or null)
+int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const Act* dyhat_out,
+                const float* dzscale = nullptr) {
+  seg_ctx* c = S.c;
+  ConvL& L = c->convs[li];
+  BnBwdArgs a{};
+  a.dz = dz.p; a.lddz = dz.ld;
+  if (z) { a.z = z->p; a.ldz = z->ld; }
+  a.y = L.y.p; a.ldy = L.y.ld; a.M = L.y.M(); a.C = L.co;
+  a.mean = L.st.mean; a.invstd = L.st.invstd; a.scale = L.st.scale;
+  a.sdy = L.st.sdy; a.sdyx = L.st.sdyx;
+  a.dy = L.dy.p; a.lddy = L.dy.ld;
+  if (dyhat_out) { a.dyhat = dyhat_out->p; a.lddyhat = dyhat_out->ld; }
+  a.part = L.bwd_part; a.rb = L.rb;
+  a.dzscale = dzscale;
+  HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
+  const bool tb = c->cfg.train_bn != 0;
+  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
+                                    tb ? c->grads + L.g_off : nullptr,
+                                    tb ? c->grads + L.b_off : nullptr, S.s));
+  HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
+  return 0;
+}
+
+// dx = dgrad(dy) [+ r1] [+ r2]
+int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr) {
+  seg_ctx* c = S.c;
+  ConvL& L = c->convs[li];
+  ConvArgs a{};
+  a.x = L.dy.p; a.N = L.N; a.H = L.Ho; a.W = L.Wo; a.C = L.co; a.ldx = L.dy.ld;
+  a.w = L.wt_lp; a.ldw = L.k * L.k * L.co;
+  a.y = dx.p; a.Ho = L.H; a.Wo = L.W; a.Co = L.ci; a.ldy = dx.ld;
+  if (r1) { a.r = r1->p; a.ldr = r1->ld; }
+  if (r2) { a.r2 = r2->p; a.ldr2 = r2->ld; }
+  a.KH = a.KW = L.k;
+  const int keff = L.k + (L.k - 1) * (L.rate - 1);
+  a.sf = 1; a.st = L.stride;
+  a.pad_h = (keff - 1) - L.pad_h; a.pad_w = (keff - 1) - L.pad_w;
+  a.dil = L.rate; a.stats = nullptr;
+  long M = (long)L.N * L.H * L.W;
+  int slot;
+  if (int r = prof_begin(c, S.s, 1, li, 2.0 * M * L.ci * L.k * L.k * L.co * 1e-9 / L.stride / L.stride, &slot)) return r;
+  HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
+  return prof_end(c, S.s, slot);
+}
+
+int conv_wgrad(Step& S, int li, const Act& x) {
+  seg_ctx* c = S.c;
+  ConvL& L = c->convs[li];
+  WgradArgs a{};
+  a.dy = L.dy.p; a.lddy = L.dy.ld;
+  a.x = x.p; a.N = x.N; a.H = x.H; a.W = x.W; a.C = x.C; a.ldx = x.ld;
+  a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co_pad;
+  a.KH = a.KW = L.k; a.sf = L.stride; a.pad_h = L.pad_h; a.pad_w = L.pad_w; a.dil = L.rate;
+  a.splits = wgrad_splits(L);
+  a.out = c->slab;
+  long P = (long)L.N * L.Ho * L.Wo;
+  int slot;
+  if (int r = prof_begin(c, S.s, 2, li, 2.0 * P * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
+  HIPCALL(c, launch_conv_wgrad(S.dt, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
+  const long n = (long)L.co * L.k * L.k * L.ci;
+  // slab rows are co_pad wide only in the Co dimension: rows 0..co-1 are the real ones
+  // split z of the slab starts at z*co_pad*ncol; rows >= co are padding and never reduced
+  HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, (long)L.co_pad * L.k * L.k * L.ci, n,
+                                  c->grads + L.w_off, 0, S.s));
+  return 0;
+}
+
+}  // namespace
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// pyramid tables
+// ------------------------------------------------------------------------------------------
+int upload_grid(seg_ctx* c, GridSpec& g, const std::vector<float>& rt, const std::vector<float>& ct) {
+  float *drt, *dct;
+  if (int r = dalloc(c, &drt, rt.size())) return r;
+  if (int r = dalloc(c, &dct, ct.size())) return r;
+  HIPCALL(c, hipMemcpy(drt, rt.data(), rt.size() * 4, hipMemcpyHostToDevice));
+  HIPCALL(c, hipMemcpy(dct, ct.data(), ct.size() * 4, hipMemcpyHostToDevice));
+  g.rowtab = drt;
+  g.coltab = dct;
+  return 0;
+}
+
+// VALID avg pools with (kh, kw) windows over an (H, W) map (remainders dropped)
+int make_pool_grids(seg_ctx* c, GridSpec& g, int H, int W, const std::vector<std::pair<int, int>>& win) {
+  memset(&g, 0, sizeof(g));
+  g.n = (int)win.size();
+  for (int i = 0; i < g.n; ++i) {
+    g.kh[i] = win[i].first; g.kw[i] = win[i].second;
+    g.kr[i] = (H - g.kh[i]) / g.kh[i] + 1;
+    g.kc[i] = (W - g.kw[i]) / g.kw[i] + 1;
+    g.ccell_off[i] = g.total_ccells; g.total_ccells += g.kc[i];
+    g.rcell_off[i] = g.total_rcells; g.total_rcells += g.kr[i];
+    g.scale[i] = 1.f / (float)(g.kh[i] * g.kw[i]);
+  }
+  if (g.total_ccells > SEG_MAX_CELLS) return set_err(&c->err, -EINVAL, "too many pyramid cells");
+  std::vector<float> rt((size_t)g.total_ccells * W, 0.f), ct((size_t)g.total_rcells * H, 0.f);
+  for (int i = 0; i < g.n; ++i) {
+    for (int j = 0; j < g.kc[i]; ++j)
+      for (int w = j * g.kw[i]; w < (j + 1) * g.kw[i]; ++w) rt[(size_t)(g.ccell_off[i] + j) * W + w] = 1.f;
+    for (int r = 0; r < g.kr[i]; ++r)
+      for (int h = r * g.kh[i]; h < (r + 1) * g.kh[i]; ++h) ct[(size_t)(g.rcell_off[i] + r) * H + h] = 1.f;
+  }
+  return upload_grid(c, g, rt, ct);
+}
+
+// transpose of an align-corners resize (kr, kc) -> (H, W)
+int make_resize_grid(seg_ctx* c, GridSpec& g, int kr, int kc, int H, int W) {
+  memset(&g, 0, sizeof(g));
+  g.n = 1; g.kr[0] = kr; g.kc[0] = kc; g.total_ccells = kc; g.total_rcells = kr; g.scale[0] = 1.f;
+  std::vector<float> rt((size_t)kc * W, 0.f), ct((size_t)kr * H, 0.f);
+  for (int w = 0; w < W; ++w) {
+    int lo, hi; float l;
+    tf_lerp_host(w, kc, W, lo, hi, l);
+    rt[(size_t)lo * W + w] += 1.f - l;
+    rt[(size_t)hi * W + w] += l;
+  }
+  for (int h = 0; h < H; ++h) {
+    int lo, hi; float l;
+    tf_lerp_host(h, kr, H, lo, hi, l);
+    ct[(size_t)lo * H + h] += 1.f - l;
+    ct[(size_t)hi * H + h] += l;
+  }
+  return upload_grid(c, g, rt, ct);
+}
+
+// ------------------------------------------------------------------------------------------
+// graph construction + allocation
+// ------------------------------------------------------------------------------------------
+int alloc_unit(seg_ctx* c, Unit& u, const Act& in) {
+  u.in = in;
+  if (u.sc >= 0)
+    if (int r = alloc_conv(c, c->convs[u.sc], in.N, in.H, in.W)) return r;
+  ConvL& c1 = c->convs[u.c1];
+  if (int r = alloc_conv(c, c1, in.N, in.H, in.W)) return r;
+  if (int r = alloc_act(c, u.z1, in.N, c1.Ho, c1.Wo, c1.co)) return r;
+  if (int r = alloc_act(c, u.dz1, in.N, c1.Ho, c1.Wo, c1.co)) return r;
+  ConvL& c2 = c->convs[u.c2];
+  if (int r = alloc_conv(c, c2, in.N, c1.Ho, c1.Wo)) return r;
+  if (int r = alloc_act(c, u.z2, in.N, c2.Ho, c2.Wo, c2.co)) return r;
+  if (int r = alloc_act(c, u.dz2, in.N, c2.Ho, c2.Wo, c2.co)) return r;
+  ConvL& c3 = c->convs[u.c3];
+  if (int r = alloc_conv(c, c3, in.N, c2.Ho, c2.Wo)) return r;
+  if (int r = alloc_act(c, u.out, in.N, c3.Ho, c3.Wo, c3.co)) return r;
+  if (int r = alloc_act(c, u.dout, in.N, c3.Ho, c3.Wo, c3.co)) return r;
+  if (u.kind != SC_CONV)
+    if (int r = alloc_act(c, u.dpre, in.N, c3.Ho, c3.Wo, c3.co)) return r;
+  return 0;
+}
+
+int build(seg_ctx* c) {
+  const seg_cfg& g = c->cfg;
+  const int N = g.nb_pp + g.nb_pb + g.nb_pi;
+  const int fd = g.feature_dims;
+  if (N <= 0 || g.height < 32 || g.width < 32) return set_err(&c->err, -EINVAL, "bad batch/size");
+  if (g.depth != 50 && g.depth != 101) return set_err(&c->err, -EINVAL, "depth must be 50|101");
+  if (g.output_stride != 8) return set_err(&c->err, -EINVAL, "output_stride must be 8");
+  if (fd % 8) return set_err(&c->err, -EINVAL, "feature_dims must be a multiple of 8");
+  const std::string rn = "feature_extractor/base/resnet_v1_" + std::to_string(g.depth);
+
+  // ---- layers in TF variable-creation order ----
+  c->stem = add_conv(c, rn + "/conv1", 3, 64, 7, 2, 1, true, true);
+  for (auto& us : resnet_units(g.depth, g.output_stride)) {
+    Unit u;
+    add_bottleneck(c, u, rn + "/" + us.scope, us.din, us.d, us.dbn, us.s, us.r);
+    c->units.push_back(u);
+  }
+  c->dfd = add_conv(c, "feature_extractor/extension/decrease_fdims", 2048, fd, 1, 1, 1, false, true);
+  if (g.pyramid == SEG_PYRAMID_PSP) {
+    const char* nm[4] = {"Conv", "Conv_1", "Conv_2", "Conv_3"};
+    for (int i = 0; i < 4; ++i)
+      c->pyr_conv.push_back(add_conv(c, std::string("feature_extractor/pyramid_module/") + nm[i], fd, fd, 1, 1, 1, false, true));
+    c->pyr_final = add_conv(c, "feature_extractor/pyramid_module/Conv_4", 5 * fd, fd, 1, 1, 1, false, true);
+  } else if (g.pyramid == SEG_PYRAMID_ASPP) {
+    return set_err(&c->err, -ENOTSUP, "ASPP pyramid not built in this version");
+  }
+  const char* hn[3] = {"l1", "l2_vehicle", "l2_human"};
+  for (int h = 0; h < 3; ++h)
+    add_bottleneck(c, c->heads[h], std::string("adaptation_module/") + hn[h] + "_features", fd, fd, fd, 1, 1);
+  fill_tables(c->tables, g.dataset);
+  c->nc[0] = c->tables.c1; c->nc[1] = c->tables.c2; c->nc[2] = c->tables.c3;
+  for (int h = 0; h < 3; ++h)
+    c->logit_conv[h] = add_conv(c, std::string("softmax_classifier/") + hn[h] + "_logits", fd, c->nc[h], 1, 1, 1, false, false);
+  c->convs[c->stem].need_dgrad = false;
+
+  // ---- flat parameter layout ----
+  long off = 0;
+  for (auto& L : c->convs) { L.w_off = off; off += (long)L.co * L.k * L.k * L.ci; }
+  c->n_decay = off;
+  for (auto& L : c->convs) { L.g_off = off; off += L.co; L.b_off = off; off += L.co; }
+  c->n_train = off;
+  long moff = 0;
+  for (auto& L : c->convs) { L.mv_off = moff; moff += L.co; }
+  c->n_moving = 2 * moff;
+  c->n_stats = c->n_moving;
+  for (auto& L : c->convs) {
+    c->pinfo.push_back({L.name + "/weights", L.w_off, (long)L.co * L.k * L.k * L.ci, SEG_PARAM_WEIGHTS, {L.co, L.k, L.k, L.ci}});
+    c->pinfo.push_back({L.name + "/BatchNorm/beta", L.b_off, L.co, SEG_PARAM_BETA, {L.co, 1, 1, 1}});
+    c->pinfo.push_back({L.name + "/BatchNorm/gamma", L.g_off, L.co, SEG_PARAM_GAMMA, {L.co, 1, 1, 1}});
+    c->pinfo.push_back({L.name + "/BatchNorm/moving_mean", L.mv_off, L.co, SEG_PARAM_MOVING_MEAN, {L.co, 1, 1, 1}});
+    c->pinfo.push_back({L.name + "/BatchNorm/moving_variance", moff + L.mv_off, L.co, SEG_PARAM_MOVING_VAR, {L.co, 1, 1, 1}});
+  }
+
+  // ---- activations ----
+  const int H = g.height, W = g.width;
+  if (c->dt == SEG_BF16)
+    if (int r = alloc_act(c, c->img, N, H, W, 3)) return r;
+  c->img.N = N; c->img.H = H; c->img.W = W; c->img.C = 3; c->img.ld = 3;
+  ConvL& st = c->convs[c->stem];
+  if (int r = alloc_conv(c, st, N, H, W)) return r;
+  if (int r = alloc_act(c, c->z0, N, st.Ho, st.Wo, 64)) return r;
+  if (int r = alloc_act(c, c->dz0, N, st.Ho, st.Wo, 64)) return r;
+  {  // max_pool2d 3x3/2 SAME
+    int Ho = (st.Ho + 1) / 2, Wo = (st.Wo + 1) / 2;
+    int th = std::max((Ho - 1) * 2 + 3 - st.Ho, 0), tw = std::max((Wo - 1) * 2 + 3 - st.Wo, 0);
+    c->pool_ph = th / 2; c->pool_pw = tw / 2;
+    if (int r = alloc_act(c, c->p0, N, Ho, Wo, 64)) return r;
+    if (int r = alloc_act(c, c->dp0, N, Ho, Wo, 64)) return r;
+  }
+  Act x = c->p0;
+  for (auto& u : c->units) {
+    if (int r = alloc_unit(c, u, x)) return r;
+    x = u.out;
+  }
+  ConvL& dfd = c->convs[c->dfd];
+  if (int r = alloc_conv(c, dfd, N, x.H, x.W)) return r;
+  const int Hf = dfd.Ho, Wf = dfd.Wo;
+  if (int r = alloc_act(c, c->dz_dfd, N, Hf, Wf, fd)) return r;
+  if (g.pyramid == SEG_PYRAMID_PSP) {
+    if (int r = alloc_act(c, c->concat, N, Hf, Wf, 5 * fd)) return r;
+    if (int r = alloc_act(c, c->dconcat, N, Hf, Wf, 5 * fd)) return r;
+    c->z_dfd = slice(c, c->concat, 0, fd);
+    // _create_psp_module: spatial dims = (hf, wf) // stride; kernel = stride = dims // k
+    const int sh = H / g.output_stride, sw = W / g.output_stride;
+    std::vector<std::pair<int, int>> win;
+    for (int k : {1, 2, 3, 6}) win.push_back({sh / k, sw / k});
+    if (int r = make_pool_grids(c, c->pool_grids, Hf, Wf, win)) return r;
+    size_t gp = (size_t)N * Hf * c->pool_grids.total_ccells * fd;
+    for (int b = 0; b < 4; ++b) {
+      const int kr = c->pool_grids.kr[b], kc = c->pool_grids.kc[b];
+      Act pa, dpa, za, dza;
+      if (int r = alloc_act(c, pa, N, kr, kc, fd)) return r;
+      if (int r = alloc_act(c, dpa, N, kr, kc, fd)) return r;
+      if (int r = alloc_act(c, za, N, kr, kc, fd)) return r;
+      if (int r = alloc_act(c, dza, N, kr, kc, fd)) return r;
+      c->pooled.push_back(pa); c->dpooled.push_back(dpa); c->zb.push_back(za); c->dzb.push_back(dza);
+      if (int r = alloc_conv(c, c->convs[c->pyr_conv[b]], N, kr, kc)) return r;
+      GridSpec ug;
+      if (int r = make_resize_grid(c, ug, kr, kc, Hf, Wf)) return r;
+      c->up_grids.push_back(ug);
+      gp = std::max(gp, (size_t)N * Hf * kc * fd);
+    }
+    if (int r = dalloc(c, &c->grid_part, gp)) return r;
+    if (int r = alloc_conv(c, c->convs[c->pyr_final], N, Hf, Wf)) return r;
+    if (int r = alloc_act(c, c->feat, N, Hf, Wf, fd)) return r;
+    if (int r = alloc_act(c, c->dfeat, N, Hf, Wf, fd)) return r;
+  } else {
+    if (int r = alloc_act(c, c->z_dfd, N, Hf, Wf, fd)) return r;
+    c->feat = c->z_dfd;
+    c->dfeat = c->dz_dfd;
+  }
+  for (int h = 0; h < 3; ++h) {
+    if (int r = alloc_unit(c, c->heads[h], c->feat)) return r;
+    if (int r = alloc_conv(c, c->convs[c->logit_conv[h]], N, Hf, Wf)) return r;
+  }
+  c->ldl = ((c->nc[0] + c->nc[1] + c->nc[2] + 3) / 4) * 4;
+  if (int r = alloc_act(c, c->logits, N, Hf, Wf, c->nc[0] + c->nc[1] + c->nc[2], c->ldl, 4)) return r;
+  if (int r = dalloc(c, &c->grad_un, (size_t)N * Hf * Wf * c->ldl)) return r;
+  c->loss_blocks = loss_head_blocks(N, Hf, Wf);
+  if (int r = dalloc(c, &c->loss_part, (size_t)c->loss_blocks * 8)) return r;
+  if (int r = dalloc(c, &c->loss_out, 16)) return r;
+  if (int r = dalloc(c, &c->dzscale, c->ldl)) return r;
+  if (int r = dalloc(c, &c->reg_part, sgdm_blocks(c->n_decay))) return r;
+  if (int r = dalloc(c, &c->reg_out, 4)) return r;
+
+  // ---- compute weight copies and workspace ----
+  if (c->dt == SEG_BF16)
+    if (int r = dalloc(c, (bf16_t**)&c->w_lp_flat, c->n_decay)) return r;
+  size_t slab = 0;
+  for (auto& L : c->convs) {
+    if (L.need_dgrad) {
+      char* p;
+      if (int r = dalloc(c, &p, (size_t)L.co * L.k * L.k * L.ci * c->esz)) return r;
+      L.wt_lp = p;
+    }
+    if (c->dt == SEG_BF16) L.w_lp = (bf16_t*)c->w_lp_flat + L.w_off;
+    slab = std::max(slab, (size_t)wgrad_splits(L) * L.co_pad * L.k * L.k * L.ci);
+  }
+  c->slab_floats = slab;
+  if (int r = dalloc(c, &c->slab, slab)) return r;
+  if (int r = dalloc(c, &c->stat_scratch, std::max<size_t>(c->stat_scratch_floats, 16))) return r;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// step
+// ------------------------------------------------------------------------------------------
+int unit_forward(Step& S, Unit& u) {
+  seg_ctx* c = S.c;
+  if (u.sc >= 0)
+    if (int r = conv_forward(S, u.sc, u.in)) return r;
+  if (int r = conv_forward(S, u.c1, u.in)) return r;
+  if (int r = bn_apply(S, u.c1, u.z1, 0)) return r;
+  if (int r = conv_forward(S, u.c2, u.z1)) return r;
+  if (int r = bn_apply(S, u.c2, u.z2, 0)) return r;
+  if (int r = conv_forward(S, u.c3, u.z2)) return r;
+  // out = relu(shortcut + bn3(conv3))
+  if (u.kind == SC_CONV) return bn_apply(S, u.c3, u.out, 0, nullptr, 1, u.sc, 1);
+  (void)c;
+  return bn_apply(S, u.c3, u.out, 0, &u.in, u.kind == SC_SUBSAMPLE ? u.stride : 1, -1, 1);
+}
+
+int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
+  seg_ctx* c = S.c;
+  const Act* dpre = u.kind != SC_CONV ? &u.dpre : nullptr;
+  if (int r = bn_backward(S, u.c3, u.dout, 0, &u.out, dpre)) return r;
+  if (u.kind == SC_CONV)
+    if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
+  if (int r = conv_wgrad(S, u.c3, u.z2)) return r;
+  if (int r = conv_dgrad(S, u.c3, u.dz2)) return r;
+  if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr)) return r;
+  if (int r = conv_wgrad(S, u.c2, u.z1)) return r;
+  if (int r = conv_dgrad(S, u.c2, u.dz1)) return r;
+  if (int r = bn_backward(S, u.c1, u.dz1, 0, &u.z1, nullptr)) return r;
+  if (int r = conv_wgrad(S, u.c1, u.in)) return r;
+  switch (u.kind) {
+    case SC_IDENTITY:
+      if (accumulate) return conv_dgrad(S, u.c1, dx, &dx, &u.dpre);
+      return conv_dgrad(S, u.c1, dx, &u.dpre);
+    case SC_SUBSAMPLE: {
+      if (accumulate) return set_err(&c->err, -EINVAL, "accumulating subsample unit");
+      if (int r = conv_dgrad(S, u.c1, dx)) return r;
+      HIPCALL(c, launch_add_strided(S.dt, dx.p, dx.H, dx.W, dx.ld, u.dpre.p, u.dpre.N, u.dpre.H,
+                                    u.dpre.W, u.dpre.C, u.dpre.ld, u.stride, S.s));
+      return 0;
+    }
+    case SC_CONV:
+      if (int r = conv_wgrad(S, u.sc, u.in)) return r;
+      if (int r = conv_dgrad(S, u.c1, dx, accumulate ? &dx : nullptr)) return r;
+      return conv_dgrad(S, u.sc, dx, &dx);
+  }
+  return 0;
+}
+
+Act logits_slice(seg_ctx* c, int h) {
+  int off = 0;
+  for (int i = 0; i < h; ++i) off += c->nc[i];
+  Act a = c->logits;
+  a.p = (float*)c->logits.p + off;
+  a.C = c->nc[h];
+  return a;
+}
+
+int forward(Step& S, const float* images) {
+  seg_ctx* c = S.c;
+  if (c->dt == SEG_BF16) {
+    HIPCALL(c, launch_cast_f32_bf16(images, (bf16_t*)c->img.p, c->img.M() * 3, S.s));
+  } else {
+    c->img.p = (void*)images;
+  }
+  if (int r = conv_forward(S, c->stem, c->img)) return r;
+  if (int r = bn_apply(S, c->stem, c->z0, 0)) return r;
+  HIPCALL(c, launch_maxpool_fwd(S.dt, c->z0.p, c->z0.N, c->z0.H, c->z0.W, 64, c->z0.ld, c->p0.p,
+                                c->p0.H, c->p0.W, c->p0.ld, c->pool_ph, c->pool_pw, S.s));
+  for (auto& u : c->units)
+    if (int r = unit_forward(S, u)) return r;
+  if (int r = conv_forward(S, c->dfd, c->units.back().out)) return r;
+  if (int r = bn_apply(S, c->dfd, c->z_dfd, 0)) return r;
+  if (c->cfg.pyramid == SEG_PYRAMID_PSP) {
+    const Act& z = c->z_dfd;
+    HIPCALL(c, launch_grid_rowreduce(S.dt, z.p, z.N, z.H, z.W, z.C, z.ld, c->pool_grids,
+                                     c->grid_part, S.s));
+    void* outs[SEG_MAX_GRIDS];
+    for (int b = 0; b < 4; ++b) outs[b] = c->pooled[b].p;
+    HIPCALL(c, launch_grid_colreduce(S.dt, c->grid_part, z.N, z.H, z.W, z.C, c->pool_grids, outs, S.s));
+    const int fd = c->cfg.feature_dims;
+    for (int b = 0; b < 4; ++b) {
+      if (int r = conv_forward(S, c->pyr_conv[b], c->pooled[b])) return r;
+      if (int r = bn_apply(S, c->pyr_conv[b], c->zb[b], 0)) return r;
+      Act dst = slice(c, c->concat, (b + 1) * fd, fd);
+      HIPCALL(c, launch_resize_fwd(S.dt, c->zb[b].p, c->zb[b].N, c->zb[b].H, c->zb[b].W, fd,
+                                   c->zb[b].ld, dst.p, dst.H, dst.W, dst.ld, S.s));
+    }
+    if (int r = conv_forward(S, c->pyr_final, c->concat)) return r;
+    if (int r = bn_apply(S, c->pyr_final, c->feat, 0)) return r;
+  }
+  for (int h = 0; h < 3; ++h) {
+    if (int r = unit_forward(S, c->heads[h])) return r;
+    if (int r = conv_forward(S, c->logit_conv[h], c->heads[h].out)) return r;
+    if (int r = bn_apply(S, c->logit_conv[h], logits_slice(c, h), 1)) return r;
+  }
+  return 0;
+}
+
+int backward(Step& S) {
+  seg_ctx* c = S.c;
+  for (int h = 0; h < 3; ++h) {
+    Act gz = logits_slice(c, h);
+    int off = (int)((float*)gz.p - (float*)c->logits.p);
+    gz.p = c->grad_un + off;
+    if (int r = bn_backward(S, c->logit_conv[h], gz, 1, nullptr, nullptr, c->dzscale + off)) return r;
+    if (int r = conv_wgrad(S, c->logit_conv[h], c->heads[h].out)) return r;
+    if (int r = conv_dgrad(S, c->logit_conv[h], c->heads[h].dout)) return r;
+    if (int r = unit_backward(S, c->heads[h], c->dfeat, h > 0)) return r;
+  }
+  if (c->cfg.pyramid == SEG_PYRAMID_PSP) {
+    const int fd = c->cfg.feature_dims;
+    if (int r = bn_backward(S, c->pyr_final, c->dfeat, 0, &c->feat, nullptr)) return r;
+    if (int r = conv_wgrad(S, c->pyr_final, c->concat)) return r;
+    if (int r = conv_dgrad(S, c->pyr_final, c->dconcat)) return r;
+    for (int b = 0; b < 4; ++b) {
+      Act d = slice(c, c->dconcat, (b + 1) * fd, fd);
+      HIPCALL(c, launch_grid_rowreduce(S.dt, d.p, d.N, d.H, d.W, fd, d.ld, c->up_grids[b],
+                                       c->grid_part, S.s));
+      void* outs[SEG_MAX_GRIDS] = {c->dzb[b].p, nullptr, nullptr, nullptr};
+      HIPCALL(c, launch_grid_colreduce(S.dt, c->grid_part, d.N, d.H, d.W, fd, c->up_grids[b], outs, S.s));
+      if (int r = bn_backward(S, c->pyr_conv[b], c->dzb[b], 0, &c->zb[b], nullptr)) return r;
+      if (int r = conv_wgrad(S, c->pyr_conv[b], c->pooled[b])) return r;
+      if (int r = conv_dgrad(S, c->pyr_conv[b], c->dpooled[b])) return r;
+    }
+    const void* dps[SEG_MAX_GRIDS];
+    for (int b = 0; b < 4; ++b) dps[b] = c->dpooled[b].p;
+    Act d0 = slice(c, c->dconcat, 0, fd);
+    HIPCALL(c, launch_psp_input_bwd(S.dt, d0.p, d0.ld, c->pool_grids, dps, d0.N, d0.H, d0.W, fd,
+                                    c->dz_dfd.p, c->dz_dfd.ld, S.s));
+  }
+  if (int r = bn_backward(S, c->dfd, c->dz_dfd, 0, &c->z_dfd, nullptr)) return r;
+  if (int r = conv_wgrad(S, c->dfd, c->units.back().out)) return r;
+  if (int r = conv_dgrad(S, c->dfd, c->units.back().dout)) return r;
+  for (int i = (int)c->units.size() - 1; i >= 0; --i) {
+    const Act& dx = i == 0 ? c->dp0 : c->units[i - 1].dout;
+    if (int r = unit_backward(S, c->units[i], dx, false)) return r;
+  }
+  HIPCALL(c, launch_maxpool_bwd(S.dt, c->z0.p, c->z0.N, c->z0.H, c->z0.W, 64, c->z0.ld, c->dp0.p,
+                                c->dp0.H, c->dp0.W, c->dp0.ld, c->dz0.p, c->dz0.ld, c->pool_ph,
+                                c->pool_pw, S.s));
+  if (int r = bn_backward(S, c->stem, c->dz0, 0, &c->z0, nullptr)) return r;
+  return conv_wgrad(S, c->stem, c->img);
+}
+
+int refresh_compute_weights(seg_ctx* c, hipStream_t s) {
+  if (c->dt == SEG_BF16)
+    HIPCALL(c, launch_cast_f32_bf16(c->params, (bf16_t*)c->w_lp_flat, c->n_decay, s));
+  for (auto& L : c->convs)
+    if (L.wt_lp)
+      HIPCALL(c, launch_weight_flip_transpose(c->dt, L.w_lp, L.wt_lp, L.co, L.k, L.k, L.ci, s));
+  return 0;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C ABI
+// ==========================================================================================
+extern "C" {
+
+const char* seg_last_error(seg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int seg_create(int device, const seg_cfg* cfg, seg_ctx** out) {
+  if (!cfg || !out) return set_err(nullptr, -EINVAL, "null argument");
+  *out = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return set_err(nullptr, -ENODEV, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+  seg_ctx* c = new seg_ctx();
+  c->cfg = *cfg;
+  c->device = device;
+  c->dt = cfg->dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32;
+  c->esz = c->dt == SEG_BF16 ? 2 : 4;
+  int r = build(c);
+  if (r) {
+    std::string msg = c->err;
+    seg_destroy(c);
+    return set_err(nullptr, r, "%s", msg.c_str());
+  }
+  *out = c;
+  return 0;
+}
+
+int seg_destroy(seg_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  for (void* p : c->allocs) (void)hipFree(p);
+  for (auto ev : c->prof.ev) (void)hipEventDestroy(ev);
+  delete c;
+  return 0;
+}
+
+int seg_sizes(seg_ctx* c, int64_t* n_train, int64_t* n_decay, int64_t* n_moving, int64_t* n_stats) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (n_train) *n_train = c->n_train;
+  if (n_decay) *n_decay = c->n_decay;
+  if (n_moving) *n_moving = c->n_moving;
+  if (n_stats) *n_stats = c->n_stats;
+  return 0;
+}
+
+int seg_bind_buffers(seg_ctx* c, float* params, float* grads, float* momentum, float* ema,
+                     float* moving) {
+  if (!c || !params || !grads || !momentum || !moving)
+    return set_err(c ? &c->err : nullptr, -EINVAL, "params/grads/momentum/moving required");
+  c->params = params; c->grads = grads; c->mom = momentum; c->ema = ema; c->moving = moving;
+  const long half = c->n_moving / 2;
+  for (auto& L : c->convs) {
+    if (c->dt == SEG_F32) L.w_lp = params + L.w_off;
+    // batch statistics land directly in the gradient tail (one all-reduce covers them)
+    L.st.mean = grads + c->n_train + L.mv_off;
+    L.st.var_unb = grads + c->n_train + half + L.mv_off;
+  }
+  c->bound = true;
+  return 0;
+}
+
+int64_t seg_param_count(seg_ctx* c) { return c ? (int64_t)c->pinfo.size() : -1; }
+
+int seg_param_info(seg_ctx* c, int64_t i, const char** name, int64_t* offset, int64_t* numel,
+                   int* kind) {
+  if (!c || i < 0 || i >= (int64_t)c->pinfo.size()) return set_err(c ? &c->err : nullptr, -EINVAL, "bad index");
+  const auto& p = c->pinfo[i];
+  if (name) *name = p.name.c_str();
+  if (offset) *offset = p.off;
+  if (numel) *numel = p.numel;
+  if (kind) *kind = p.kind;
+  return 0;
+}
+
+int seg_param_shape(seg_ctx* c, int64_t i, int64_t* dims) {
+  if (!c || !dims || i < 0 || i >= (int64_t)c->pinfo.size())
+    return set_err(c ? &c->err : nullptr, -EINVAL, "bad index");
+  for (int k = 0; k < 4; ++k) dims[k] = c->pinfo[i].dims[k];
+  return 0;
+}
+
+#define NEED_BOUND(c) \
+  if (!(c) || !(c)->bound) return set_err((c) ? &(c)->err : nullptr, -EINVAL, "context not bound")
+
+int seg_params_updated(seg_ctx* c, void* stream) {
+  NEED_BOUND(c);
+  return refresh_compute_weights(c, (hipStream_t)stream);
+}
+
+int seg_forward(seg_ctx* c, const float* images, void* stream) {
+  NEED_BOUND(c);
+  if (!images) return set_err(&c->err, -EINVAL, "images required");
+  Step S{c, (hipStream_t)stream, c->dt};
+  return forward(S, images);
+}
+
+int seg_loss(seg_ctx* c, const int32_t* px, const float* bbox, const float* tag, int32_t* decisions,
+             void* stream) {
+  NEED_BOUND(c);
+  const seg_cfg& g = c->cfg;
+  if ((g.nb_pp && !px) || (g.nb_pb && !bbox) || (g.nb_pi && !tag))
+    return set_err(&c->err, -EINVAL, "missing labels for a non-empty sub-batch");
+  LossArgs a{};
+  a.logits = (const float*)c->logits.p; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
+  a.ldl = c->ldl; a.H = g.height; a.W = g.width;
+  a.npp = g.nb_pp; a.npb = g.nb_pb; a.npi = g.nb_pi;
+  a.px_labels = px; a.bbox_soft = bbox; a.tag_soft = tag;
+  a.grad_un = c->grad_un; a.part = c->loss_part; a.decisions = decisions;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCALL(c, launch_loss_head(a, c->tables, s));
+  HIPCALL(c, launch_loss_finalize(c->loss_part, c->loss_blocks, c->tables, c->ldl, c->loss_out,
+                                  c->dzscale, s));
+  return 0;
+}
+
+int seg_backward(seg_ctx* c, void* stream) {
+  NEED_BOUND(c);
+  Step S{c, (hipStream_t)stream, c->dt};
+  return backward(S);
+}
+
+int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, float grad_scale,
+                     void* stream) {
+  NEED_BOUND(c);
+  hipStream_t s = (hipStream_t)stream;
+  if (grad_scale != 1.f)
+    HIPCALL(c, launch_scale_inplace(c->grads, c->n_train + c->n_stats, grad_scale, s));
+  SgdmArgs a{};
+  a.w = c->params; a.g = c->grads; a.v = c->mom;
+  a.ema = ema_decay_eff > 0.f ? c->ema : nullptr;
+  a.w_lp = c->dt == SEG_BF16 ? (bf16_t*)c->w_lp_flat : nullptr;
+  a.n = c->n_decay; a.lr = lr; a.momentum = momentum; a.wd = c->cfg.weight_decay;
+  a.ema_decay = ema_decay_eff; a.reg_part = c->reg_part;
+  HIPCALL(c, launch_sgdm(a, s));
+  HIPCALL(c, launch_sum_partials(c->reg_part, sgdm_blocks(c->n_decay), c->reg_out, s));
+  if (c->cfg.train_bn) {
+    SgdmArgs b = a;
+    b.w = c->params + c->n_decay; b.g = c->grads + c->n_decay; b.v = c->mom + c->n_decay;
+    b.ema = a.ema ? c->ema + c->n_decay : nullptr; b.w_lp = nullptr; b.n = c->n_train - c->n_decay;
+    b.wd = 0.f; b.reg_part = nullptr;
+    HIPCALL(c, launch_sgdm(b, s));
+  }
+  const long half = c->n_moving / 2;
+  HIPCALL(c, launch_moving_update(c->moving, c->moving + half, c->grads + c->n_train,
+                                  c->grads + c->n_train + half, (int)half, c->cfg.bn_decay, s));
+  for (auto& L : c->convs)
+    if (L.wt_lp)
+      HIPCALL(c, launch_weight_flip_transpose(c->dt, L.w_lp, L.wt_lp, L.co, L.k, L.k, L.ci, s));
+  return 0;
+}
+
+int seg_outputs(seg_ctx* c, const float** losses, const float** reg, const float** logits,
+                int* ld, int* hl, int* wl) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (losses) *losses = c->loss_out;
+  if (reg) *reg = c->reg_out;
+  if (logits) *logits = (const float*)c->logits.p;
+  if (ld) *ld = c->ldl;
+  if (hl) *hl = c->logits.H;
+  if (wl) *wl = c->logits.W;
+  return 0;
+}
+
+int seg_confusion(seg_ctx* c, const int32_t* labels, const int32_t* decisions, int64_t n,
+                  int num_classes, int32_t* cm, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(cm, 0, (size_t)num_classes * num_classes * 4, s);
+  if (e == hipSuccess) e = launch_confusion(labels, decisions, n, num_classes, cm, s);
+  if (e != hipSuccess) return hip_fail(c, e, "seg_confusion");
+  return 0;
+}
+
+int seg_profile(seg_ctx* c, int enable) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (enable && c->prof.ev.empty()) {
+    c->prof.ev.resize(16384);
+    for (auto& ev : c->prof.ev) HIPCALL(c, hipEventCreate(&ev));
+  }
+  c->prof.on = enable != 0;
+  c->prof.recs.clear();
+  c->prof.next = 0;
+  return 0;
+}
+
+int seg_profile_read(seg_ctx* c, int cls, double* ms_total, double* gflop_total,
+                     int64_t* launches, double* ms_max_layer, char* layer_name, int name_len) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  double tot = 0, gf = 0;
+  int64_t n = 0;
+  std::vector<double> per_layer(c->convs.size(), 0.0);
+  for (auto& r : c->prof.recs) {
+    if (r.cls != cls) continue;
+    HIPCALL(c, hipEventSynchronize(c->prof.ev[r.e1]));
+    float ms = 0;
+    HIPCALL(c, hipEventElapsedTime(&ms, c->prof.ev[r.e0], c->prof.ev[r.e1]));
+    tot += ms; gf += r.gflop; ++n;
+    per_layer[r.layer] += ms;
+  }
+  int best = -1;
+  for (size_t i = 0; i < per_layer.size(); ++i)
+    if (best < 0 || per_layer[i] > per_layer[best]) best = (int)i;
+  if (ms_total) *ms_total = tot;
+  if (gflop_total) *gflop_total = gf;
+  if (launches) *launches = n;
+  if (ms_max_layer) *ms_max_layer = best >= 0 ? per_layer[best] : 0;
+  if (layer_name && name_len > 0) {
+    snprintf(layer_name, name_len, "%s", best >= 0 ? c->convs[best].name.c_str() : "");
+  }
+  return 0;
+}
+
+static void op_geom(int H, int W, int k, int stride, int rate, int explicit_pad, int* Ho, int* Wo,
+                    int* ph, int* pw) {
+  ConvL L;
+  L.k = k; L.stride = stride; L.rate = rate; L.explicit_pad = explicit_pad != 0;
+  conv_geom(L, 1, H, W);
+  *Ho = L.Ho; *Wo = L.Wo; *ph = L.pad_h; *pw = L.pad_w;
+}
+
+int seg_op_conv_fwd(int dtype, const void* x, int N, int H, int W, int C, int ldx, const void* w,
+                    int Co, int k, int stride, int rate, int explicit_pad, void* y, int ldy,
+                    float* stats, void* stream) {
+  int Ho, Wo, ph, pw;
+  op_geom(H, W, k, stride, rate, explicit_pad, &Ho, &Wo, &ph, &pw);
+  ConvArgs a{};
+  a.x = x; a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx;
+  a.w = w; a.ldw = k * k * C; a.y = y; a.Ho = Ho; a.Wo = Wo; a.Co = Co; a.ldy = ldy;
+  a.KH = a.KW = k; a.sf = stride; a.st = 1; a.pad_h = ph; a.pad_w = pw; a.dil = rate; a.stats = stats;
+  hipError_t e = launch_conv_nt(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, 0, a, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_fwd");
+}
+
+int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
+                      const void* wt, int Ci, int k, int stride, int rate, int explicit_pad, int H,
+                      int W, void* dx, int lddx, void* stream) {
+  int ho, wo, ph, pw;
+  op_geom(H, W, k, stride, rate, explicit_pad, &ho, &wo, &ph, &pw);
+  if (ho != Ho || wo != Wo) return set_err(nullptr, -EINVAL, "dgrad geometry mismatch");
+  const int keff = k + (k - 1) * (rate - 1);
+  ConvArgs a{};
+  a.x = dy; a.N = N; a.H = Ho; a.W = Wo; a.C = Co; a.ldx = lddy;
+  a.w = wt; a.ldw = k * k * Co; a.y = dx; a.Ho = H; a.Wo = W; a.Co = Ci; a.ldy = lddx;
+  a.KH = a.KW = k; a.sf = 1; a.st = stride; a.pad_h = keff - 1 - ph; a.pad_w = keff - 1 - pw;
+  a.dil = rate;
+  hipError_t e = launch_conv_nt(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, 0, a, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_dgrad");
+}
+
+int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
+                      const void* x, int H, int W, int Ci, int ldx, int k, int stride, int rate,
+                      int explicit_pad, float* dw, void* workspace, int64_t ws_bytes, void* stream) {
+  int ho, wo, ph, pw;
+  op_geom(H, W, k, stride, rate, explicit_pad, &ho, &wo, &ph, &pw);
+  if (ho != Ho || wo != Wo) return set_err(nullptr, -EINVAL, "wgrad geometry mismatch");
+  ConvL L;
+  L.co_pad = Co; L.co = Co; L.ci = Ci; L.k = k; L.N = N; L.Ho = Ho; L.Wo = Wo;
+  WgradArgs a{};
+  a.dy = dy; a.lddy = lddy; a.x = x; a.N = N; a.H = H; a.W = W; a.C = Ci; a.ldx = ldx;
+  a.Ho = Ho; a.Wo = Wo; a.Co = Co; a.KH = a.KW = k; a.sf = stride; a.pad_h = ph; a.pad_w = pw;
+  a.dil = rate; a.splits = wgrad_splits(L);
+  const long n = (long)Co * k * k * Ci;
+  if ((int64_t)a.splits * n * 4 > ws_bytes) a.splits = (int)std::max<int64_t>(1, ws_bytes / (n * 4));
+  a.out = (float*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = launch_conv_wgrad(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, a, s);
+  if (e == hipSuccess) e = launch_splitk_reduce((float*)workspace, a.splits, n, n, dw, 0, s);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_wgrad");
+}
+
+}  // extern "C"

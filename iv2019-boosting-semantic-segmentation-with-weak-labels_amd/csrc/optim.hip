@@ -1,0 +1,92 @@
+// Optimizer kernels (see optim.h).
+#include "optim.h"
+
+namespace {
+
+constexpr int SG_THREADS = 256;
+constexpr int SG_PER_BLOCK = SG_THREADS * 16;
+
+__global__ void sgdm_kernel(SgdmArgs a) {
+  const long base = (long)blockIdx.x * SG_PER_BLOCK;
+  float reg = 0.f;
+  for (int k = 0; k < 16; ++k) {
+    const long i = base + (long)k * SG_THREADS + threadIdx.x;
+    if (i >= a.n) break;
+    const float w_old = a.w[i];
+    reg += w_old * w_old;
+    // total gradient = d(seg)/dw + d(wd * sum(w^2)/2)/dw
+    const float gt = a.g[i] + a.wd * w_old;
+    // tf.train.MomentumOptimizer (use_nesterov=False): accum = accum*m + g; var -= lr*accum
+    const float v = a.v[i] * a.momentum + gt;
+    a.v[i] = v;
+    const float w_new = w_old - a.lr * v;
+    a.w[i] = w_new;
+    if (a.ema) a.ema[i] -= (1.f - a.ema_decay) * (a.ema[i] - w_old);
+    if (a.w_lp) a.w_lp[i] = f2bf(w_new);
+  }
+  if (a.reg_part) {
+    __shared__ float sh[SG_THREADS / 64];
+    float s = wave_sum(reg);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int q = 0; q < SG_THREADS / 64; ++q) t += sh[q];
+      a.reg_part[blockIdx.x] = 0.5f * a.wd * t;
+    }
+  }
+}
+
+__global__ void sum_partials_kernel(const float* __restrict__ p, int n, float* out) {
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += p[i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) sh[threadIdx.x] += sh[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = (float)sh[0];
+}
+
+__global__ void cast_kernel(const float* __restrict__ s, bf16_t* __restrict__ d, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    d[i] = f2bf(s[i]);
+}
+
+__global__ void scale_kernel(float* x, long n, float f) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    x[i] *= f;
+}
+
+}  // namespace
+
+int sgdm_blocks(long n) { return ceil_div(n, SG_PER_BLOCK); }
+
+hipError_t launch_sgdm(const SgdmArgs& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sgdm_kernel, dim3(sgdm_blocks(a.n)), dim3(SG_THREADS), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_partials(const float* part, int n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, part, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast_f32_bf16(const float* src, bf16_t* dst, long n, hipStream_t s) {
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(cast_kernel, dim3((int)g), dim3(256), 0, s, src, dst, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale_inplace(float* x, long n, float f, hipStream_t s) {
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(scale_kernel, dim3((int)g), dim3(256), 0, s, x, n, f);
+  return hipGetLastError();
+}

@@ -1,0 +1,45 @@
+// Pooling, subsampling, pyramid (PSP/ASPP) pooling and align-corners bilinear resize.
+#pragma once
+#include "seg_common.h"
+
+// Separable "grid reduction" spec: for pyramid pools (VALID avg pool, kernel = stride) and
+// for the transpose of an align_corners bilinear resize from a small k x k grid.
+#define SEG_MAX_GRIDS 4
+#define SEG_MAX_CELLS 24
+struct GridSpec {
+  int n;                          // number of grids
+  int kr[SEG_MAX_GRIDS];          // grid rows (cells along H)
+  int kc[SEG_MAX_GRIDS];          // grid cols (cells along W)
+  int kh[SEG_MAX_GRIDS];          // avg-pool window (psp_input_bwd only)
+  int kw[SEG_MAX_GRIDS];
+  int ccell_off[SEG_MAX_GRIDS];   // first column-cell of grid g in a row's cell list
+  int rcell_off[SEG_MAX_GRIDS];   // first row-cell of grid g in coltab
+  int total_ccells;               // sum_g kc[g]
+  int total_rcells;               // sum_g kr[g]
+  float scale[SEG_MAX_GRIDS];     // output scale per grid (1/(kh*kw) for avg pool)
+  const float* rowtab;            // device [total_ccells][W]: weight of column w for cell
+  const float* coltab;            // device [total_rcells][H]: weight of row h for cell
+};
+
+hipError_t launch_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+                              void* y, int Ho, int Wo, int ldy, int pad_h, int pad_w,
+                              hipStream_t s);
+hipError_t launch_maxpool_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+                              const void* dy, int Ho, int Wo, int lddy, void* dx, int lddx,
+                              int pad_h, int pad_w, hipStream_t s);
+// dx[n][ho*s][wo*s][c] += g[n][ho][wo][c]
+hipError_t launch_add_strided(int dtype, void* dx, int H, int W, int lddx, const void* g, int N,
+                              int Ho, int Wo, int C, int ldg, int stride, hipStream_t s);
+// rows pass: part[n][h][cell][c] = sum_w x[n][h][w][c] * weight(g, w, cell)
+hipError_t launch_grid_rowreduce(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+                                 const GridSpec& g, float* part, hipStream_t s);
+// cols pass: out_g[n][i][j][c] = scale * sum_h part[n][h][cell(g,j)][c] * weight(g, h, i)
+hipError_t launch_grid_colreduce(int dtype, const float* part, int N, int H, int W, int C,
+                                 const GridSpec& g, void* const* outs, hipStream_t s);
+// align_corners bilinear resize small [N][k][k][C] -> [N][Ho][Wo] slice (ld)
+hipError_t launch_resize_fwd(int dtype, const void* x, int N, int hi, int wi, int C, int ldx,
+                             void* y, int Ho, int Wo, int ldy, hipStream_t s);
+// dx = dconcat_slice + sum_g avgpool_bwd(dpooled_g)   (PSP input gradient)
+hipError_t launch_psp_input_bwd(int dtype, const void* dcat, int ldcat, const GridSpec& g,
+                                const void* const* dpooled, int N, int H, int W, int C, void* dx,
+                                int lddx, hipStream_t s);

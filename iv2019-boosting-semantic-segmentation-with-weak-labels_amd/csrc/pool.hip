@@ -1,0 +1,361 @@
+// Pooling / pyramid / resize kernels (see pool.h). 8-channel vectors (16 B bf16, 32 B f32)
+// per thread; channel counts here are always multiples of 8 (checked by the launchers).
+#include "pool.h"
+
+namespace {
+
+inline int grid_for(long items) {
+  long g = (items + 255) / 256;
+  return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
+}
+
+// ---- max pool 3x3 stride 2, TF SAME padding (pads are -inf, i.e. ignored) ---------------
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W, int C, int ldx,
+                                   T* __restrict__ y, int Ho, int Wo, int ldy, int ph, int pw) {
+  const int cg_n = C / 8;
+  const long total = (long)N * Ho * Wo * cg_n;
+  for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+       it += (long)gridDim.x * blockDim.x) {
+    int cg = (int)(it % cg_n);
+    long p = it / cg_n;
+    int wo = (int)(p % Wo);
+    long t = p / Wo;
+    int ho = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    float mx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
+    for (int dh = 0; dh < 3; ++dh) {
+      int hi = ho * 2 - ph + dh;
+      if (hi < 0 || hi >= H) continue;
+      for (int dw = 0; dw < 3; ++dw) {
+        int wi = wo * 2 - pw + dw;
+        if (wi < 0 || wi >= W) continue;
+        float v[8];
+        Vec8<T>::load(x + ((size_t)((long)n * H + hi) * W + wi) * ldx + cg * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mx[e] = v[e] > mx[e] ? v[e] : mx[e];
+      }
+    }
+    Vec8<T>::store(y + ((size_t)((long)n * Ho + ho) * Wo + wo) * ldy + cg * 8, mx);
+  }
+}
+
+// gather form: each input pixel sums the gradients of the windows whose first max it is
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ x, int N, int H, int W, int C, int ldx,
+                                   const T* __restrict__ dy, int Ho, int Wo, int lddy,
+                                   T* __restrict__ dx, int lddx, int ph, int pw) {
+  const int cg_n = C / 8;
+  const long total = (long)N * H * W * cg_n;
+  for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+       it += (long)gridDim.x * blockDim.x) {
+    int cg = (int)(it % cg_n);
+    long p = it / cg_n;
+    int wi = (int)(p % W);
+    long t = p / W;
+    int hi = (int)(t % H);
+    int n = (int)(t / H);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    int ho_lo = (hi + ph - 2 + 1) >> 1;  // ceil((hi+ph-2)/2) for hi+ph-2 >= -1
+    if (hi + ph - 2 < 0) ho_lo = 0;
+    int ho_hi = (hi + ph) >> 1;
+    int wo_lo = (wi + pw - 2 + 1) >> 1;
+    if (wi + pw - 2 < 0) wo_lo = 0;
+    int wo_hi = (wi + pw) >> 1;
+    for (int ho = ho_lo; ho <= ho_hi && ho < Ho; ++ho) {
+      for (int wo = wo_lo; wo <= wo_hi && wo < Wo; ++wo) {
+        // first max of window (ho, wo) per channel
+        float mx[8];
+        int arg[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { mx[e] = -INFINITY; arg[e] = -1; }
+        for (int dh = 0; dh < 3; ++dh) {
+          int h2 = ho * 2 - ph + dh;
+          if (h2 < 0 || h2 >= H) continue;
+          for (int dw = 0; dw < 3; ++dw) {
+            int w2 = wo * 2 - pw + dw;
+            if (w2 < 0 || w2 >= W) continue;
+            float v[8];
+            Vec8<T>::load(x + ((size_t)((long)n * H + h2) * W + w2) * ldx + cg * 8, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (v[e] > mx[e]) { mx[e] = v[e]; arg[e] = dh * 3 + dw; }
+          }
+        }
+        const int me = (hi - (ho * 2 - ph)) * 3 + (wi - (wo * 2 - pw));
+        float g[8];
+        Vec8<T>::load(dy + ((size_t)((long)n * Ho + ho) * Wo + wo) * lddy + cg * 8, g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (arg[e] == me) acc[e] += g[e];
+      }
+    }
+    Vec8<T>::store(dx + ((size_t)((long)n * H + hi) * W + wi) * lddx + cg * 8, acc);
+  }
+}
+
+template <typename T>
+__global__ void add_strided_kernel(T* __restrict__ dx, int H, int W, int lddx, const T* __restrict__ g,
+                                   int N, int Ho, int Wo, int C, int ldg, int s) {
+  const int cg_n = C / 8;
+  const long total = (long)N * Ho * Wo * cg_n;
+  for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+       it += (long)gridDim.x * blockDim.x) {
+    int cg = (int)(it % cg_n);
+    long p = it / cg_n;
+    int wo = (int)(p % Wo);
+    long t = p / Wo;
+    int ho = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    T* d = dx + ((size_t)((long)n * H + ho * s) * W + wo * s) * lddx + cg * 8;
+    float a[8], b[8];
+    Vec8<T>::load(d, a);
+    Vec8<T>::load(g + (size_t)p * ldg + cg * 8, b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] += b[e];
+    Vec8<T>::store(d, a);
+  }
+}
+
+// ---- separable grid reductions ------------------------------------------------------------
+// block per (n, h); thread per channel; registers indexed statically by cell q
+template <typename T>
+__global__ void grid_rowreduce_kernel(const T* __restrict__ x, int N, int H, int W, int C, int ldx,
+                                      GridSpec g, float* __restrict__ part) {
+  const int n = blockIdx.x / H, h = blockIdx.x % H;
+  __shared__ float tab[SEG_MAX_CELLS * 256];
+  for (int cbase = 0; cbase < C; cbase += blockDim.x) {
+    const int c = cbase + threadIdx.x;
+    const bool act = c < C;
+    float acc[SEG_MAX_CELLS];
+#pragma unroll
+    for (int q = 0; q < SEG_MAX_CELLS; ++q) acc[q] = 0.f;
+    const T* row = x + (size_t)((long)n * H + h) * W * ldx + (act ? c : 0);
+    for (int w0 = 0; w0 < W; w0 += 256) {
+      const int wn = (W - w0) < 256 ? (W - w0) : 256;
+      __syncthreads();
+      for (int i = threadIdx.x; i < g.total_ccells * wn; i += blockDim.x) {
+        int q = i / wn, w = i % wn;
+        tab[q * 256 + w] = g.rowtab[(size_t)q * W + w0 + w];
+      }
+      __syncthreads();
+      for (int w = 0; w < wn && act; ++w) {
+        float v = ldf(row + (size_t)(w0 + w) * ldx);
+#pragma unroll
+        for (int q = 0; q < SEG_MAX_CELLS; ++q)
+          if (q < g.total_ccells) acc[q] += v * tab[q * 256 + w];
+      }
+    }
+    float* o = part + (size_t)((long)n * H + h) * g.total_ccells * C + c;
+#pragma unroll
+    for (int q = 0; q < SEG_MAX_CELLS; ++q)
+      if (act && q < g.total_ccells) o[(size_t)q * C] = acc[q];
+  }
+}
+
+struct OutPtrs { void* p[SEG_MAX_GRIDS]; };
+
+template <typename T>
+__global__ void grid_colreduce_kernel(const float* __restrict__ part, int N, int H, int C,
+                                      GridSpec g, OutPtrs outs) {
+  // output element enumeration: grid by grid, [n][i][j][c]
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int gi = 0; gi < g.n; ++gi) {
+    long cnt = (long)N * g.kr[gi] * g.kc[gi] * C;
+    if (idx < cnt) {
+      int c = (int)(idx % C);
+      long t = idx / C;
+      int j = (int)(t % g.kc[gi]);
+      t /= g.kc[gi];
+      int i = (int)(t % g.kr[gi]);
+      int n = (int)(t / g.kr[gi]);
+      const int qi = g.rcell_off[gi] + i, qj = g.ccell_off[gi] + j;
+      float s = 0.f;
+      for (int h = 0; h < H; ++h) {
+        float wgt = g.coltab[(size_t)qi * H + h];
+        if (wgt != 0.f) s += wgt * part[((size_t)((long)n * H + h) * g.total_ccells + qj) * C + c];
+      }
+      stf((T*)outs.p[gi] + idx, s * g.scale[gi]);
+      return;
+    }
+    idx -= cnt;
+  }
+}
+
+// ---- align-corners bilinear resize (TF legacy scaler, TF lerp form) ------------------------
+__device__ __forceinline__ void tf_lerp(int o, int n_in, int n_out, int& lo, int& hi, float& l) {
+  float scale = n_out > 1 ? (float)(n_in - 1) / (float)(n_out - 1) : 0.f;
+  float fin = (float)o * scale;
+  lo = (int)fin;
+  hi = lo + 1 < n_in - 1 ? lo + 1 : n_in - 1;
+  l = fin - (float)lo;
+}
+
+template <typename T>
+__global__ void resize_fwd_kernel(const T* __restrict__ x, int N, int hi_n, int wi_n, int C,
+                                  int ldx, T* __restrict__ y, int Ho, int Wo, int ldy) {
+  const int cg_n = C / 8;
+  const long total = (long)N * Ho * Wo * cg_n;
+  for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+       it += (long)gridDim.x * blockDim.x) {
+    int cg = (int)(it % cg_n);
+    long p = it / cg_n;
+    int wo = (int)(p % Wo);
+    long t = p / Wo;
+    int ho = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    int y0, y1, x0, x1;
+    float yl, xl;
+    tf_lerp(ho, hi_n, Ho, y0, y1, yl);
+    tf_lerp(wo, wi_n, Wo, x0, x1, xl);
+    const T* base = x + (size_t)n * hi_n * wi_n * ldx + cg * 8;
+    float tl[8], tr[8], bl[8], br[8], o[8];
+    Vec8<T>::load(base + ((size_t)y0 * wi_n + x0) * ldx, tl);
+    Vec8<T>::load(base + ((size_t)y0 * wi_n + x1) * ldx, tr);
+    Vec8<T>::load(base + ((size_t)y1 * wi_n + x0) * ldx, bl);
+    Vec8<T>::load(base + ((size_t)y1 * wi_n + x1) * ldx, br);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float top = tl[e] + (tr[e] - tl[e]) * xl;
+      float bot = bl[e] + (br[e] - bl[e]) * xl;
+      o[e] = top + (bot - top) * yl;
+    }
+    Vec8<T>::store(y + (size_t)p * ldy + cg * 8, o);
+  }
+}
+
+struct InPtrs { const void* p[SEG_MAX_GRIDS]; };
+
+template <typename T>
+__global__ void psp_input_bwd_kernel(const T* __restrict__ dcat, int ldcat, GridSpec g, InPtrs dp,
+                                     int N, int H, int W, int C, T* __restrict__ dx, int lddx) {
+  const int cg_n = C / 8;
+  const long total = (long)N * H * W * cg_n;
+  for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+       it += (long)gridDim.x * blockDim.x) {
+    int cg = (int)(it % cg_n);
+    long p = it / cg_n;
+    int w = (int)(p % W);
+    long t = p / W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    float a[8];
+    Vec8<T>::load(dcat + (size_t)p * ldcat + cg * 8, a);
+    for (int gi = 0; gi < g.n; ++gi) {
+      int i = h / g.kh[gi], j = w / g.kw[gi];
+      if (i < g.kr[gi] && j < g.kc[gi]) {
+        float b[8];
+        const T* src = (const T*)dp.p[gi] + ((size_t)((long)n * g.kr[gi] + i) * g.kc[gi] + j) * C + cg * 8;
+        Vec8<T>::load(src, b);
+        const float sc = g.scale[gi];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += b[e] * sc;
+      }
+    }
+    Vec8<T>::store(dx + (size_t)p * lddx + cg * 8, a);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+                              void* y, int Ho, int Wo, int ldy, int pad_h, int pad_w,
+                              hipStream_t s) {
+  if (C % 8 || ldx % 8 || ldy % 8) return hipErrorInvalidValue;
+  dim3 g(grid_for((long)N * Ho * Wo * C / 8));
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, N, H, W, C,
+                       ldx, (bf16_t*)y, Ho, Wo, ldy, pad_h, pad_w);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, dim3(256), 0, s, (const float*)x, N, H, W, C,
+                       ldx, (float*)y, Ho, Wo, ldy, pad_h, pad_w);
+  return hipGetLastError();
+}
+
+hipError_t launch_maxpool_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+                              const void* dy, int Ho, int Wo, int lddy, void* dx, int lddx,
+                              int pad_h, int pad_w, hipStream_t s) {
+  if (C % 8 || ldx % 8 || lddy % 8 || lddx % 8) return hipErrorInvalidValue;
+  dim3 g(grid_for((long)N * H * W * C / 8));
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, N, H, W, C,
+                       ldx, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, pad_h, pad_w);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, dim3(256), 0, s, (const float*)x, N, H, W, C,
+                       ldx, (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, pad_h, pad_w);
+  return hipGetLastError();
+}
+
+hipError_t launch_add_strided(int dtype, void* dx, int H, int W, int lddx, const void* g, int N,
+                              int Ho, int Wo, int C, int ldg, int stride, hipStream_t s) {
+  if (C % 8 || lddx % 8 || ldg % 8) return hipErrorInvalidValue;
+  dim3 gr(grid_for((long)N * Ho * Wo * C / 8));
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(add_strided_kernel<bf16_t>, gr, dim3(256), 0, s, (bf16_t*)dx, H, W, lddx,
+                       (const bf16_t*)g, N, Ho, Wo, C, ldg, stride);
+  else
+    hipLaunchKernelGGL(add_strided_kernel<float>, gr, dim3(256), 0, s, (float*)dx, H, W, lddx,
+                       (const float*)g, N, Ho, Wo, C, ldg, stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_grid_rowreduce(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+                                 const GridSpec& g, float* part, hipStream_t s) {
+  if (g.total_ccells > SEG_MAX_CELLS) return hipErrorInvalidValue;
+  dim3 gr(N * H);
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(grid_rowreduce_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)x, N, H,
+                       W, C, ldx, g, part);
+  else
+    hipLaunchKernelGGL(grid_rowreduce_kernel<float>, gr, dim3(256), 0, s, (const float*)x, N, H, W,
+                       C, ldx, g, part);
+  return hipGetLastError();
+}
+
+hipError_t launch_grid_colreduce(int dtype, const float* part, int N, int H, int W, int C,
+                                 const GridSpec& g, void* const* outs, hipStream_t s) {
+  (void)W;
+  OutPtrs o;
+  long total = 0;
+  for (int i = 0; i < SEG_MAX_GRIDS; ++i) o.p[i] = i < g.n ? outs[i] : nullptr;
+  for (int i = 0; i < g.n; ++i) total += (long)N * g.kr[i] * g.kc[i] * C;
+  dim3 gr(ceil_div(total, 256));
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(grid_colreduce_kernel<bf16_t>, gr, dim3(256), 0, s, part, N, H, C, g, o);
+  else
+    hipLaunchKernelGGL(grid_colreduce_kernel<float>, gr, dim3(256), 0, s, part, N, H, C, g, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_resize_fwd(int dtype, const void* x, int N, int hi, int wi, int C, int ldx,
+                             void* y, int Ho, int Wo, int ldy, hipStream_t s) {
+  if (C % 8 || ldx % 8 || ldy % 8) return hipErrorInvalidValue;
+  dim3 gr(grid_for((long)N * Ho * Wo * C / 8));
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(resize_fwd_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)x, N, hi, wi,
+                       C, ldx, (bf16_t*)y, Ho, Wo, ldy);
+  else
+    hipLaunchKernelGGL(resize_fwd_kernel<float>, gr, dim3(256), 0, s, (const float*)x, N, hi, wi, C,
+                       ldx, (float*)y, Ho, Wo, ldy);
+  return hipGetLastError();
+}
+
+hipError_t launch_psp_input_bwd(int dtype, const void* dcat, int ldcat, const GridSpec& g,
+                                const void* const* dpooled, int N, int H, int W, int C, void* dx,
+                                int lddx, hipStream_t s) {
+  if (C % 8 || ldcat % 8 || lddx % 8) return hipErrorInvalidValue;
+  InPtrs ip;
+  for (int i = 0; i < SEG_MAX_GRIDS; ++i) ip.p[i] = i < g.n ? dpooled[i] : nullptr;
+  dim3 gr(grid_for((long)N * H * W * C / 8));
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(psp_input_bwd_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)dcat, ldcat,
+                       g, ip, N, H, W, C, (bf16_t*)dx, lddx);
+  else
+    hipLaunchKernelGGL(psp_input_bwd_kernel<float>, gr, dim3(256), 0, s, (const float*)dcat, ldcat, g,
+                       ip, N, H, W, C, (float*)dx, lddx);
+  return hipGetLastError();
+}

@@ -1,0 +1,84 @@
+"""Drop-in ``define_estimator`` (estimator/define_estimator_hierarchical.py:39-239).
+
+Signature kept: ``define_estimator(mode, features, labels, model_fn, config, params)`` is
+bound with ``functools.partial(define_estimator, model_fn=...)`` by the facade exactly as in
+system_factory.py:178-187. Instead of a TF graph it runs the step eagerly on the device:
+
+  model_fn forward  ->  define_losses (fused loss head)  ->  train_op():
+      backward (HIP)  ->  gradient all-reduce over RCCL when distributed  ->
+      fused SGDM + L2 + BN moving averages + EMA (HIP)
+
+The returned ``EstimatorSpec`` holds ``train_op``, a callable that finishes the step.
+Gradient semantics follow TF 1.12 MirroredStrategy: every rank normalises its
+loss by its own non-zero-weight counts; gradients are averaged across ranks (SUM all-reduce
+then 1/N); BN batch statistics (for the moving averages) are averaged the same way. EMA is
+disabled when distributed (system_factory.py:236-238).
+"""
+from __future__ import annotations
+
+from collections import namedtuple
+
+from estimator.define_losses_hierarchical import define_losses
+from estimator.define_optimizer import define_optimizer
+from estimator.mode_keys import ModeKeys
+
+EstimatorSpec = namedtuple('EstimatorSpec', ['mode', 'predictions', 'loss', 'train_op', 'losses'])
+
+
+class GlobalStep(object):
+    def __init__(self, value=0):
+        self.value = int(value)
+
+
+_GLOBAL_STEP = GlobalStep()
+
+
+def get_or_create_global_step():
+    return _GLOBAL_STEP
+
+
+def world_size():
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def allreduce_grads(ctx):
+    """SUM all-reduce of the flat gradient buffer (gradients + BN batch-statistics tail) over
+    the process group (RCCL over xGMI on MI355X; gloo on CPU tests). Returns the scale that
+    turns the sum into the tower mean."""
+    import torch.distributed as dist
+    n = world_size()
+    if n > 1:
+        dist.all_reduce(ctx.grads, op=dist.ReduceOp.SUM)
+    return 1.0 / n
+
+
+def ema_decay_effective(ema_decay, step):
+    """tf.train.ExponentialMovingAverage(decay, num_updates=global_step)."""
+    if not ema_decay or ema_decay <= 0:
+        return 0.0
+    return min(ema_decay, (1.0 + step) / (10.0 + step))
+
+
+def define_estimator(mode, features, labels, model_fn, config, params):
+    assert mode in (ModeKeys.TRAIN, ModeKeys.EVAL, ModeKeys.PREDICT)
+    assert params.name_feature_extractor in {'resnet_v1_50', 'resnet_v1_101'}
+    proimages = features['proimages']
+    _, _, predictions = model_fn(mode, proimages, labels, config, params)
+    if mode != ModeKeys.TRAIN:
+        raise NotImplementedError('EVAL/PREDICT are out of scope of the native training path')
+    global_step = get_or_create_global_step()
+    losses = define_losses(mode, predictions, labels, config, params)
+    optimizer = define_optimizer(global_step, params)
+    ctx = predictions['_context']
+
+    def train_op():
+        ctx.backward()
+        scale = allreduce_grads(ctx)
+        ema = 0.0 if world_size() > 1 else ema_decay_effective(params.ema_decay, global_step.value)
+        ctx.apply_update(optimizer.learning_rate(global_step.value), optimizer.momentum,
+                         ema, scale)
+        global_step.value += 1
+        return losses
+
+    return EstimatorSpec(mode, predictions, losses['total'], train_op, losses)

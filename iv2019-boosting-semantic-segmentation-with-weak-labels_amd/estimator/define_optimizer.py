@@ -1,0 +1,58 @@
+"""Learning-rate schedules + optimizer selection, drop-in for estimator/define_optimizer.py.
+
+The update itself is the fused HIP kernel (``seg_apply_update``); this module resolves the
+per-step learning rate exactly as tf.train.piecewise_constant / polynomial_decay do, and the
+momentum (MomentumOptimizer) or 0 (GradientDescentOptimizer).
+"""
+from dataclasses import dataclass
+from typing import List
+
+
+@dataclass
+class Optimizer:
+    schedule: str
+    boundaries: List[int]
+    values: List[float]
+    initial: float
+    final: float
+    power: float
+    decay_steps: int
+    momentum: float
+    use_nesterov: bool
+
+    def learning_rate(self, global_step: int) -> float:
+        if self.schedule == 'piecewise_constant':
+            # tf.train.piecewise_constant: values[i] for boundaries[i-1] < step <= boundaries[i]
+            for b, v in zip(self.boundaries, self.values):
+                if global_step <= b:
+                    return float(v)
+            return float(self.values[len(self.boundaries)])
+        # tf.train.polynomial_decay (cycle=False)
+        step = min(global_step, self.decay_steps)
+        frac = 1.0 - step / float(self.decay_steps)
+        return float((self.initial - self.final) * frac ** self.power + self.final)
+
+    # reference code reads optimizer._learning_rate for summaries
+    @property
+    def _learning_rate(self):
+        return self.learning_rate
+
+
+def define_optimizer(global_step, params):
+    if params.use_nesterov if hasattr(params, 'use_nesterov') else False:
+        raise NotImplementedError('use_nesterov: the fused update implements plain momentum only')
+    if params.learning_rate_schedule not in ('piecewise_constant', 'polynomial_decay'):
+        print('Unknown option for learning rate schedule.')
+    if params.optimizer == 'SGDM':
+        momentum = params.momentum
+    elif params.optimizer == 'SGD':
+        momentum = 0.0
+    else:
+        assert False, 'Unknown option for optimizer.'
+    return Optimizer(schedule=params.learning_rate_schedule,
+                     boundaries=list(getattr(params, 'learning_rate_boundaries', []) or []),
+                     values=list(getattr(params, 'learning_rate_values', []) or []),
+                     initial=params.learning_rate_initial,
+                     final=params.learning_rate_final, power=params.learning_rate_power,
+                     decay_steps=max(int(getattr(params, 'num_training_steps', 1)), 1),
+                     momentum=momentum, use_nesterov=False)

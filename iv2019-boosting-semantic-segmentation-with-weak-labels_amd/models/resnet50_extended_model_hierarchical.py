@@ -1,0 +1,116 @@
+"""Drop-in ``model_fn`` of the reference (models/resnet50_extended_model_hierarchical.py).
+
+``model(mode, features, labels, config, params)`` keeps the reference signature and
+return value ``(features, end_points, predictions)``. The network itself is not built in
+Python: the native context (``seg_hip.SegContext``, one per device per process) holds the
+dilated ResNet-50/101 encoder, the PSP pyramid, the three adaptation bottlenecks and the
+logits convs, and this function runs its forward pass on the device tensor ``features``
+(``proimages``, NHWC fp32 in [-1, 1)).
+
+``predictions`` carries the LOW-RESOLUTION logits (the 8x align-corners upsampling of
+hierarchical.py:84-86 is fused into the loss head, which never materialises full-resolution
+logits); ``decisions`` is the full-resolution fused decision map filled by the loss head.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from estimator.mode_keys import ModeKeys
+from input_pipelines.utils import get_temp_Nb
+from models.initializers import init_params
+
+_CONTEXTS = {}
+
+
+def _validate_params(params):
+    # hierarchical.py:272-276
+    if bool(getattr(params, 'fov_expansion_kernel_rate', 0)) != bool(
+            getattr(params, 'fov_expansion_kernel_size', 0)):
+        raise ValueError("One of params.{fov_expansion_kernel_rate, fov_expansion_kernel_size} "
+                         "is set. In order to take effect both should be set.")
+    if getattr(params, 'fov_expansion_kernel_size', 0):
+        raise NotImplementedError('increase_fov conv is not built by the native path')
+    if getattr(params, 'upsampling_method', 'bilinear') != 'bilinear':
+        raise NotImplementedError("only upsampling_method='bilinear' (the default) is fused")
+    if getattr(params, 'norm_layer', 'batch') != 'batch':
+        raise NotImplementedError("only norm_layer='batch' is implemented")
+    if getattr(params, 'stride_feature_extractor', 8) != 8:
+        raise NotImplementedError('stride_feature_extractor must be 8')
+
+
+def sub_batches(config, params):
+    """Per-rank (per-tower) sub-batches: each of the three is split (get_temp_Nb)."""
+    return (get_temp_Nb(config, getattr(params, 'Nb_per_pixel', params.Nb)),
+            get_temp_Nb(config, getattr(params, 'Nb_per_bbox', 0)),
+            get_temp_Nb(config, getattr(params, 'Nb_per_image', 0)))
+
+
+def get_context(config, params, device=None):
+    """The process's native context for these settings (created on first use)."""
+    from seg_hip import SegContext
+    import torch
+    nb_pp, nb_pb, nb_pi = sub_batches(config, params)
+    depth = 101 if getattr(params, 'name_feature_extractor', 'resnet_v1_50') == 'resnet_v1_101' else 50
+    pyramid = getattr(params, 'pyramid', None) or ('psp' if getattr(params, 'psp_module', False) else 'none')
+    dev = torch.cuda.current_device() if device is None else device
+    key = (dev, depth, pyramid, params.height_feature_extractor, params.width_feature_extractor,
+           nb_pp, nb_pb, nb_pi, getattr(params, 'compute_dtype', 'bf16'),
+           params.per_pixel_dataset_name)
+    ctx = _CONTEXTS.get(key)
+    if ctx is None:
+        ctx = SegContext(depth=depth, pyramid=pyramid, height=params.height_feature_extractor,
+                         width=params.width_feature_extractor, nb_pp=nb_pp, nb_pb=nb_pb,
+                         nb_pi=nb_pi, dtype=getattr(params, 'compute_dtype', 'bf16'),
+                         dataset=params.per_pixel_dataset_name,
+                         feature_dims=getattr(params, 'feature_dims_decreased', 256),
+                         bn_decay=getattr(params, 'batch_norm_decay', 0.9),
+                         train_bn=getattr(params, 'norm_train_variables', True),
+                         weight_decay=getattr(params, 'regularization_weight', 0.00017),
+                         ema=getattr(params, 'ema_decay', 0) > 0, device=dev)
+        ctx.load_params(init_params(ctx.param_info, seed=getattr(params, 'init_seed', 0)))
+        _CONTEXTS[key] = ctx
+    return ctx
+
+
+def model(mode, features, labels, config, params):
+    """Forward pass (hierarchical.py:17-141). ``features``: device tensor [N, hf, wf, 3]."""
+    import torch
+    _validate_params(params)
+    if mode != ModeKeys.TRAIN:
+        raise NotImplementedError('EVAL/PREDICT forward (moving-statistics BN) is out of scope '
+                                  'for the native training path (SURVEY §2 #15/#16)')
+    ctx = get_context(config, params)
+    assert features.shape[-1] == 3, 'features must be NHWC with 3 channels'
+    ctx.forward(features.contiguous())
+    _, _, logits = ctx.outputs()
+    c1, c2, c3 = (53, 12, 5) if params.per_pixel_dataset_name == 'vistas' else (14, 7, 3)
+    n = features.shape[0]
+    decisions = torch.zeros((n, params.height_feature_extractor, params.width_feature_extractor),
+                            dtype=torch.int32, device=features.device)
+    predictions = {'l1_logits': logits[..., :c1],
+                   'l2_vehicle_logits': logits[..., c1:c1 + c2],
+                   'l2_human_logits': logits[..., c1 + c2:c1 + c2 + c3],
+                   'decisions': decisions,
+                   '_context': ctx}
+    return None, {}, predictions
+
+
+def add_model_arguments(argparser):
+    """Same flags and defaults as hierarchical.py:228-269."""
+    a = argparser.add_argument
+    a('--stride_feature_extractor', type=int, default=8)
+    a('--name_feature_extractor', type=str, default='resnet_v1_50',
+      choices=['resnet_v1_50', 'resnet_v1_101'])
+    a('--feature_dims_decreased', type=int, default=256)
+    a('--fov_expansion_kernel_size', type=int, default=0)
+    a('--fov_expansion_kernel_rate', type=int, default=0)
+    a('--upsampling_method', type=str, default='bilinear', choices=['no', 'bilinear', 'hybrid'])
+    a('--psp_module', action='store_true')
+    a('--norm_layer', type=str, default='batch', choices=['batch', 'group'])
+    a('--cross_replica_norm', action='store_true')
+    a('--norm_train_variables', action='store_true')
+    a('--batch_norm_accumulate_statistics', action='store_true')
+    a('--batch_norm_decay', type=float, default=0.9)
+    # build-side additions
+    a('--compute_dtype', type=str, default='bf16', choices=['bf16', 'fp32'])
+    a('--init_seed', type=int, default=0)

@@ -1,0 +1,257 @@
+"""ctypes binding of ``libseg_hip.so`` (C ABI in ``include/seg_hip.h``).
+
+This is the only way the host code reaches the GPU path. There is no fallback: if the
+library is missing or does not load, importing this module raises ``RuntimeError``.
+PyTorch is used only for device memory (flat parameter buffers, inputs) and the stream
+handle; every kernel of the training step is in the HIP library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libseg_hip.so")
+
+EXPORTED_SYMBOLS = [
+    "seg_create", "seg_destroy", "seg_last_error", "seg_sizes", "seg_bind_buffers",
+    "seg_param_count", "seg_param_info", "seg_param_shape", "seg_params_updated", "seg_forward", "seg_loss",
+    "seg_backward", "seg_apply_update", "seg_outputs", "seg_confusion", "seg_profile",
+    "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_dgrad", "seg_op_conv_wgrad",
+]
+
+PYRAMID = {"none": 0, "psp": 1, "aspp": 2}
+DTYPE = {"fp32": 0, "bf16": 1}
+DATASET = {"cityscapes": 0, "vistas": 1}
+PARAM_KIND = {0: "weights", 1: "gamma", 2: "beta", 3: "moving_mean", 4: "moving_variance"}
+
+
+class SegCfg(ctypes.Structure):
+    _fields_ = [
+        ("depth", ctypes.c_int), ("pyramid", ctypes.c_int), ("height", ctypes.c_int),
+        ("width", ctypes.c_int), ("nb_pp", ctypes.c_int), ("nb_pb", ctypes.c_int),
+        ("nb_pi", ctypes.c_int), ("dtype", ctypes.c_int), ("dataset", ctypes.c_int),
+        ("output_stride", ctypes.c_int), ("feature_dims", ctypes.c_int),
+        ("bn_decay", ctypes.c_float), ("train_bn", ctypes.c_int),
+        ("weight_decay", ctypes.c_float),
+    ]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libseg_hip.so not found at {LIB_PATH}: build it with __graft_entry__.build() "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        raise RuntimeError(f"failed to load {LIB_PATH}: {e}") from e
+    vp, ip, i64, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+    sig = {
+        "seg_create": (ip, [ip, ctypes.POINTER(SegCfg), ctypes.POINTER(vp)]),
+        "seg_destroy": (ip, [vp]),
+        "seg_last_error": (ctypes.c_char_p, [vp]),
+        "seg_sizes": (ip, [vp] + [ctypes.POINTER(i64)] * 4),
+        "seg_bind_buffers": (ip, [vp, vp, vp, vp, vp, vp]),
+        "seg_param_count": (i64, [vp]),
+        "seg_param_info": (ip, [vp, i64, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(i64),
+                                ctypes.POINTER(i64), ctypes.POINTER(ip)]),
+        "seg_param_shape": (ip, [vp, i64, ctypes.POINTER(i64)]),
+        "seg_params_updated": (ip, [vp, vp]),
+        "seg_forward": (ip, [vp, vp, vp]),
+        "seg_loss": (ip, [vp, vp, vp, vp, vp, vp]),
+        "seg_backward": (ip, [vp, vp]),
+        "seg_apply_update": (ip, [vp, f, f, f, f, vp]),
+        "seg_outputs": (ip, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                             ctypes.POINTER(ip), ctypes.POINTER(ip), ctypes.POINTER(ip)]),
+        "seg_confusion": (ip, [vp, vp, vp, i64, ip, vp, vp]),
+        "seg_profile": (ip, [vp, ip]),
+        "seg_profile_read": (ip, [vp, ip, ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ip]),
+        "seg_op_conv_fwd": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, vp, ip, vp, vp]),
+        "seg_op_conv_dgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, vp,
+                                   ip, vp]),
+        "seg_op_conv_wgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, ip,
+                                   vp, vp, i64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+LIB = _load()
+
+
+def check(rc: int, ctx=None):
+    if rc != 0:
+        msg = LIB.seg_last_error(ctx)
+        raise RuntimeError(f"libseg_hip error {rc}: {msg.decode() if msg else ''}")
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+@dataclass
+class ParamInfo:
+    name: str
+    offset: int
+    numel: int
+    kind: str
+    shape: tuple
+
+
+class SegContext:
+    """One device context of the native training path (one per GPU per process).
+
+    Owns the flat fp32 buffers (as torch tensors on the context's device): ``params``,
+    ``grads`` (+ BN batch-statistics tail), ``momentum``, optional ``ema`` and ``moving``.
+    """
+
+    def __init__(self, *, depth=50, pyramid="psp", height=512, width=1024, nb_pp=2, nb_pb=0,
+                 nb_pi=0, dtype="bf16", dataset="cityscapes", output_stride=8,
+                 feature_dims=256, bn_decay=0.9, train_bn=True, weight_decay=0.00017,
+                 ema=False, device=None):
+        import torch
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.cfg = SegCfg(depth, PYRAMID[pyramid], height, width, nb_pp, nb_pb, nb_pi,
+                          DTYPE[dtype], DATASET[dataset], output_stride, feature_dims,
+                          bn_decay, int(bool(train_bn)), weight_decay)
+        self.dtype = dtype
+        h = ctypes.c_void_p()
+        check(LIB.seg_create(self.device.index, ctypes.byref(self.cfg), ctypes.byref(h)))
+        self.h = h
+        vals = [ctypes.c_int64() for _ in range(4)]
+        check(LIB.seg_sizes(self.h, *[ctypes.byref(v) for v in vals]), self.h)
+        self.n_train, self.n_decay, self.n_moving, self.n_stats = [v.value for v in vals]
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.params = torch.zeros(self.n_train, **f32)
+        self.grads = torch.zeros(self.n_train + self.n_stats, **f32)
+        self.momentum = torch.zeros(self.n_train, **f32)
+        self.ema = torch.zeros(self.n_train, **f32) if ema else None
+        self.moving = torch.zeros(self.n_moving, **f32)
+        check(LIB.seg_bind_buffers(self.h, _ptr(self.params), _ptr(self.grads),
+                                   _ptr(self.momentum), _ptr(self.ema), _ptr(self.moving)), self.h)
+        self.param_info = self._param_info()
+
+    # ---- parameters -----------------------------------------------------------------
+    def _param_info(self) -> List[ParamInfo]:
+        out = []
+        for i in range(LIB.seg_param_count(self.h)):
+            nm, off, n, k = ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+            check(LIB.seg_param_info(self.h, i, ctypes.byref(nm), ctypes.byref(off),
+                                     ctypes.byref(n), ctypes.byref(k)), self.h)
+            dims = (ctypes.c_int64 * 4)()
+            check(LIB.seg_param_shape(self.h, i, dims), self.h)
+            kind = PARAM_KIND[k.value]
+            shape = tuple(dims) if kind == "weights" else (dims[0],)
+            out.append(ParamInfo(nm.value.decode(), off.value, n.value, kind, shape))
+        return out
+
+    def _buffer_for(self, p: ParamInfo):
+        return self.moving if p.kind in ("moving_mean", "moving_variance") else self.params
+
+    def load_params(self, values: Dict[str, np.ndarray], stream=None):
+        """Write named parameters (weights [Co][KH][KW][Ci]) and refresh compute copies."""
+        import torch
+        for p in self.param_info:
+            if p.name in values:
+                v = torch.as_tensor(np.asarray(values[p.name], dtype=np.float32).reshape(-1))
+                if v.numel() != p.numel:
+                    raise ValueError(f"{p.name}: expected {p.numel} values, got {v.numel()}")
+                self._buffer_for(p)[p.offset:p.offset + p.numel].copy_(v.to(self.device))
+        if self.ema is not None:
+            self.ema.copy_(self.params)
+        check(LIB.seg_params_updated(self.h, _stream(stream)), self.h)
+
+    def named(self, buffer: str = "params") -> Dict[str, np.ndarray]:
+        """Host copies of named tensors of params/grads/momentum/ema."""
+        buf = {"params": self.params, "grads": self.grads, "momentum": self.momentum,
+               "ema": self.ema}[buffer]
+        out = {}
+        for p in self.param_info:
+            if p.kind in ("moving_mean", "moving_variance"):
+                src = self.moving if buffer == "params" else None
+            else:
+                src = buf
+            if src is not None:
+                out[p.name] = src[p.offset:p.offset + p.numel].detach().cpu().numpy()
+        return out
+
+    # ---- step -----------------------------------------------------------------------
+    def forward(self, images, stream=None):
+        check(LIB.seg_forward(self.h, _ptr(images), _stream(stream)), self.h)
+
+    def loss(self, px_labels=None, bbox_soft=None, tag_soft=None, decisions=None, stream=None):
+        check(LIB.seg_loss(self.h, _ptr(px_labels), _ptr(bbox_soft), _ptr(tag_soft),
+                           _ptr(decisions), _stream(stream)), self.h)
+
+    def backward(self, stream=None):
+        check(LIB.seg_backward(self.h, _stream(stream)), self.h)
+
+    def apply_update(self, lr, momentum=0.9, ema_decay_eff=0.0, grad_scale=1.0, stream=None):
+        check(LIB.seg_apply_update(self.h, lr, momentum, ema_decay_eff, grad_scale,
+                                   _stream(stream)), self.h)
+
+    def outputs(self):
+        """(losses[10], reg[1], low-res logits [N,Hl,Wl,ldl]) as torch views (device)."""
+        import torch
+        l, r, lg = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        ld, hl, wl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(LIB.seg_outputs(self.h, ctypes.byref(l), ctypes.byref(r), ctypes.byref(lg),
+                              ctypes.byref(ld), ctypes.byref(hl), ctypes.byref(wl)), self.h)
+        n = self.cfg.nb_pp + self.cfg.nb_pb + self.cfg.nb_pi
+        return (_wrap(l.value, (10,), self.device), _wrap(r.value, (1,), self.device),
+                _wrap(lg.value, (n, hl.value, wl.value, ld.value), self.device))
+
+    def confusion(self, labels, decisions, num_classes, out, stream=None):
+        check(LIB.seg_confusion(self.h, _ptr(labels), _ptr(decisions), labels.numel(),
+                                num_classes, _ptr(out), _stream(stream)), self.h)
+
+    def profile(self, enable: bool):
+        check(LIB.seg_profile(self.h, int(enable)), self.h)
+
+    def profile_read(self, cls: int):
+        ms, gf, mx = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_int64()
+        name = ctypes.create_string_buffer(256)
+        check(LIB.seg_profile_read(self.h, cls, ctypes.byref(ms), ctypes.byref(gf), ctypes.byref(n),
+                                   ctypes.byref(mx), name, 256), self.h)
+        return dict(ms=ms.value, gflop=gf.value, launches=n.value, ms_max_layer=mx.value,
+                    max_layer=name.value.decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            LIB.seg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _wrap(ptr: int, shape: Tuple[int, ...], device):
+    """Zero-copy torch view of a context-owned fp32 device buffer."""
+    import torch
+
+    class _CAI:
+        pass
+    o = _CAI()
+    o.__cuda_array_interface__ = {"shape": shape, "typestr": "<f4", "data": (ptr, False),
+                                  "version": 3, "strides": None}
+    return torch.as_tensor(o, device=device)

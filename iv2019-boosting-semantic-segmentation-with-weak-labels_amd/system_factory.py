@@ -1,0 +1,203 @@
+"""Drop-in ``SemanticSegmentation`` facade (code/system_factory.py).
+
+Same constructor ``SemanticSegmentation(input_fns, model_fn, settings)``, same settings
+post-processing (problem definition, ``output_Nclasses``, learning-rate boundaries in
+epochs -> steps, defaults and validation), ``.train()`` runs the step loop on the native
+path. Data parallelism is one process per GPU (``torch.distributed``, backend 'nccl' =
+RCCL): launch with ``torchrun`` and pass ``--distribute``. ``.predict()``/``.evaluate()``
+(inference, visualisation, eval with moving-statistics BN) are out of scope.
+
+Checkpoints are ``<log_dir>/model.ckpt-<step>.pt`` state dicts (named parameters, momentum,
+moving statistics, EMA, global step); the training loop resumes from the latest one.
+"""
+from __future__ import annotations
+
+import collections
+import copy
+import functools
+import glob
+import json
+import os
+import re
+import time
+from os.path import exists, isdir, join, split
+
+from estimator.define_estimator_hierarchical import (define_estimator,
+                                                      get_or_create_global_step, world_size)
+from estimator.mode_keys import ModeKeys
+from utils.utils import _replacevoids, print_metrics_from_confusion_matrix  # noqa: F401
+
+__version__ = '0.9-mi355x'
+
+
+class DistributeConfig(object):
+    def __init__(self, num_towers):
+        self.num_towers = num_towers
+
+
+class RunConfig(object):
+    """The parts of tf.estimator.RunConfig the hot path reads (input_pipelines/utils.py:119)."""
+
+    def __init__(self, model_dir=None, save_summary_steps=120, save_checkpoints_steps=None,
+                 train_distribute=None, log_step_count_steps=120):
+        self.model_dir = model_dir
+        self.save_summary_steps = save_summary_steps
+        self.save_checkpoints_steps = save_checkpoints_steps
+        self.train_distribute = train_distribute
+        self.log_step_count_steps = log_step_count_steps
+
+
+class SemanticSegmentation(object):
+
+    def __init__(self, input_fns, model_fn, settings):
+        assert settings is not None, 'settings must be provided for now.'
+        self._settings = copy.deepcopy(settings)
+        s = self._settings
+        s.height_network = s.height_feature_extractor
+        s.width_network = s.width_feature_extractor
+        with open(s.training_problem_def_path, 'r') as fp:
+            s.training_problem_def = json.load(fp)
+        _set_defaults(s)
+        _validate_settings(s)
+        self._input_fns = input_fns
+        self._model_fn = model_fn
+        lids2cids = s.training_problem_def['lids2cids']
+        s.lids_training_contain_unlabeled = -1 in lids2cids
+        s.output_Nclasses = (max(lids2cids) + 1 +
+                             (s.lids_training_contain_unlabeled or getattr(s, 'train_void_class', False)))
+        self._estimator_fn = functools.partial(define_estimator, model_fn=self._model_fn)
+
+    @property
+    def settings(self):
+        return self._settings
+
+    # system_factory.py:189-302
+    def _prepare_train_settings(self):
+        s = self._settings
+        s.num_examples_per_epoch = int(s.Ntrain * s.height_network // s.height_feature_extractor *
+                                       s.width_network // s.width_feature_extractor)
+        s.num_batches_per_epoch = int(s.num_examples_per_epoch / s.Nb)
+        s.num_training_steps = int(s.Ne * s.num_batches_per_epoch)
+        if s.learning_rate_schedule == 'piecewise_constant':
+            if not (s.learning_rate_decay or s.learning_rate_values):
+                s.learning_rate_decay = 0.5
+            last_boundary = s.Ne - s.learning_rate_boundaries[-1]
+            if last_boundary == 0:
+                s.learning_rate_boundaries.pop()
+            elif last_boundary < 0:
+                raise ValueError('Ne is less than learning rate boundaries.')
+            s.learning_rate_boundaries_epochs = s.learning_rate_boundaries
+            s.learning_rate_boundaries = [lrb * s.num_batches_per_epoch
+                                          for lrb in s.learning_rate_boundaries]
+            if s.learning_rate_decay:
+                n = len(s.learning_rate_boundaries) + 1
+                s.learning_rate_values = [s.learning_rate_initial * s.learning_rate_decay ** i
+                                          for i in range(n)]
+        if s.distribute:
+            s.ema_decay = 0
+        if not s.save_checkpoints_steps:
+            s.save_checkpoints_steps = s.num_batches_per_epoch
+
+    def train(self, max_steps=None, log_fn=print):
+        import torch
+        s = self._settings
+        self._prepare_train_settings()
+        if s.distribute:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group(backend='nccl' if torch.cuda.is_available() else 'gloo')
+            torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', 0)))
+        rank = int(os.environ.get('RANK', 0))
+        os.makedirs(s.log_dir, exist_ok=True)
+        if rank == 0:
+            settings_filename = join(s.log_dir, 'settings.txt')
+            assert not exists(settings_filename), (
+                f"Previous settings.txt found in {s.log_dir}. Rename or delete it manually and "
+                "restart training.")
+            d = collections.OrderedDict(sorted((k, v) for k, v in vars(s).items()
+                                               if k != 'training_problem_def'))
+            with open(settings_filename, 'w') as f:
+                for k, v in enumerate(d):
+                    print(f"{k:2} : {v} : {d[v]}", file=f)
+        n = world_size()
+        config = RunConfig(model_dir=s.log_dir, save_summary_steps=s.save_summaries_steps,
+                           save_checkpoints_steps=s.save_checkpoints_steps,
+                           train_distribute=DistributeConfig(n) if n > 1 else None)
+        step = get_or_create_global_step()
+        total = s.num_training_steps if max_steps is None else min(max_steps, s.num_training_steps)
+        data = iter(self._input_fns['train'](config, s))
+        from models.resnet50_extended_model_hierarchical import get_context
+        ctx = get_context(config, s)
+        self._maybe_restore(ctx, step)
+        if rank == 0:
+            log_fn(f"training {total} steps on {n} GPU(s)")
+        t0 = time.time()
+        while step.value < total:
+            features, labels = next(data)
+            spec = self._estimator_fn(ModeKeys.TRAIN, features, labels, config=config, params=s)
+            ctx = spec.predictions['_context']
+            losses = spec.train_op()
+            if rank == 0 and (step.value % s.save_summaries_steps == 0 or step.value == total):
+                torch.cuda.synchronize()
+                log_fn(f"step {step.value}: total {float(losses['total']):.4f} "
+                       f"l1 {float(losses['l1_segmentation']):.4f} "
+                       f"l2v {float(losses['l2_vehicle_segmentation']):.4f} "
+                       f"l2h {float(losses['l2_human_segmentation']):.4f} "
+                       f"({(time.time() - t0) / max(step.value, 1):.3f} s/step)")
+            if rank == 0 and step.value % s.save_checkpoints_steps == 0:
+                self.save(ctx, step.value)
+        if rank == 0 and ctx is not None:
+            self.save(ctx, step.value)
+        return step.value
+
+    # ---- checkpoints ---------------------------------------------------------------
+    def save(self, ctx, global_step):
+        import torch
+        state = {'global_step': global_step, 'params': ctx.named('params'),
+                 'momentum': ctx.named('momentum')}
+        if ctx.ema is not None:
+            state['ema'] = ctx.named('ema')
+        torch.save(state, join(self._settings.log_dir, f'model.ckpt-{global_step}.pt'))
+
+    def _maybe_restore(self, ctx, step):
+        import torch
+        ck = sorted(glob.glob(join(self._settings.log_dir, 'model.ckpt-*.pt')),
+                    key=lambda p: int(re.findall(r'-(\d+)\.pt$', p)[0]))
+        if not ck:
+            return
+        state = torch.load(ck[-1], weights_only=True)
+        ctx.load_params(state['params'])
+        mom = state['momentum']
+        for p in ctx.param_info:
+            if p.name in mom:
+                ctx.momentum[p.offset:p.offset + p.numel].copy_(torch.as_tensor(mom[p.name]))
+        step.value = int(state['global_step'])
+
+    def predict(self):
+        raise NotImplementedError('inference/visualisation is out of scope (SURVEY §2 #15)')
+
+    def evaluate(self):
+        raise NotImplementedError('evaluation is disabled in the reference (evaluate.py:82) '
+                                  'and out of scope here')
+
+
+def _set_defaults(settings):
+    if getattr(settings, 'learning_rate_schedule', None) == 'piecewise_constant':
+        if not (settings.learning_rate_decay or settings.learning_rate_values):
+            settings.learning_rate_decay = 0.5
+
+
+def _validate_settings(settings):
+    assert settings.height_network == settings.height_feature_extractor and \
+        settings.width_network == settings.width_feature_extractor, (
+            'For now height/width_network and height/width_feature_extractor should be equal.')
+    if getattr(settings, 'learning_rate_schedule', None) == 'piecewise_constant':
+        if not (bool(settings.learning_rate_decay) != bool(settings.learning_rate_values)):
+            raise AttributeError('If `learning_rate_schedule` is `piecewise_constant` exactly one '
+                                 'of `learning_rate_decay` or `learning_rate_values` must be given.')
+    lids2cids_unique = set(settings.training_problem_def['lids2cids'])
+    cid_max = max(lids2cids_unique)
+    lids2cids_unique.discard(-1)
+    if not (lids2cids_unique == set(range(cid_max + 1))):
+        raise ValueError('lids2cids field in training problem definition contains not '
+                         'continuous class ids.')

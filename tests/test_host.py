@@ -1,0 +1,159 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every declared symbol,
+the ctypes struct mirrors the header, and the drop-in Python surface (argparse flags,
+learning-rate schedule, per-tower batch split, gradient averaging over 2 gloo ranks)."""
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "seg_hip.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(seg_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    import seg_hip
+    for name in _declared():
+        assert hasattr(seg_hip.LIB, name), name
+    assert sorted(seg_hip.EXPORTED_SYMBOLS) == _declared()
+
+
+def test_cfg_struct_matches_header():
+    import seg_hip
+    src = open(HEADER).read()
+    body = src[src.index("typedef struct seg_cfg {"):src.index("} seg_cfg;")]
+    fields = []
+    for line in body.splitlines()[1:]:
+        m = re.match(r"\s*(int|float)\s+([^;]+);", line)
+        if m:
+            fields += [n.strip() for n in m.group(2).split(",")]
+    assert [f[0] for f in seg_hip.SegCfg._fields_] == fields
+
+
+def test_train_arguments_match_reference_defaults():
+    from estimator.mode_keys import ModeKeys
+    from models.resnet50_extended_model_hierarchical import add_model_arguments
+    from utils.utils import SemanticSegmentationArguments
+    a = SemanticSegmentationArguments(mode=ModeKeys.TRAIN)
+    add_model_arguments(a.argparser)
+    s = a.parse_args(["/tmp/log", "cityscapes", "--psp_module"])
+    assert (s.Nb, s.Ne, s.learning_rate_initial, s.learning_rate_boundaries) == (4, 17, 0.01, [8, 15, 17])
+    assert (s.regularization_weight, s.momentum, s.ema_decay, s.batch_norm_decay) == (0.00017, 0.9, 0.9, 0.9)
+    assert (s.stride_feature_extractor, s.feature_dims_decreased, s.psp_module) == (8, 256, True)
+    assert (s.height_feature_extractor, s.width_feature_extractor) == (512, 1024)
+
+
+def test_learning_rate_schedule_piecewise_constant():
+    from estimator.define_optimizer import define_optimizer
+
+    class P:
+        learning_rate_schedule = "piecewise_constant"
+        learning_rate_boundaries = [10, 20]
+        learning_rate_values = [0.01, 0.005, 0.0025]
+        learning_rate_initial = 0.01
+        learning_rate_final = 0.0
+        learning_rate_power = 0.9
+        optimizer = "SGDM"
+        momentum = 0.9
+        use_nesterov = False
+    opt = define_optimizer(None, P)
+    assert [opt.learning_rate(s) for s in (0, 10, 11, 20, 21)] == [0.01, 0.01, 0.005, 0.005, 0.0025]
+    assert opt.momentum == 0.9
+
+
+def test_facade_lr_boundaries_in_epochs():
+    from system_factory import SemanticSegmentation
+    from utils.utils import SemanticSegmentationArguments
+    from models.resnet50_extended_model_hierarchical import add_model_arguments
+    a = SemanticSegmentationArguments(mode="train")
+    add_model_arguments(a.argparser)
+    s = a.parse_args(["/tmp/x", "cityscapes", "--Ntrain", "400", "--Nb", "4"])
+    s.training_problem_def_path = os.path.join(
+        REPO, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
+        "problem_definitions", "cityscapes", "problem01.json")
+    sys_ = SemanticSegmentation({}, None, s)
+    assert sys_.settings.output_Nclasses == 20
+    sys_._prepare_train_settings()
+    st = sys_.settings
+    assert st.num_batches_per_epoch == 100 and st.num_training_steps == 1700
+    assert st.learning_rate_boundaries == [800, 1500]          # last boundary == Ne is dropped
+    np.testing.assert_allclose(st.learning_rate_values, [0.01, 0.005, 0.0025])
+
+
+def test_get_temp_nb():
+    from input_pipelines.utils import get_temp_Nb
+
+    class Cfg:
+        class train_distribute:
+            num_towers = 4
+    assert get_temp_Nb(Cfg, 32) == 8
+    with pytest.raises(AssertionError):
+        get_temp_Nb(Cfg, 6)
+
+    class One:
+        train_distribute = None
+    assert get_temp_Nb(One, 6) == 6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from estimator.define_estimator_hierarchical import allreduce_grads
+
+    class Ctx:
+        grads = torch.arange(6, dtype=torch.float32) * (rank + 1)
+    scale = allreduce_grads(Ctx)
+    q.put((rank, scale, (Ctx.grads * scale).tolist()))
+    dist.destroy_process_group()
+
+
+def test_gradient_averaging_two_gloo_ranks():
+    """Per-tower gradients are SUM all-reduced then scaled by 1/N (MirroredStrategy mean)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    exp = (np.arange(6) * 1 + np.arange(6) * 2) / 2.0
+    for _, scale, g in res:
+        assert scale == 0.5
+        np.testing.assert_allclose(g, exp)
+
+
+def test_initializer_matches_oracle_scheme():
+    from models.initializers import init_params
+    from oracle.tfseg import SegConfig, build_specs, init_params as oracle_init
+
+    class PI:
+        def __init__(self, name, kind, shape, numel):
+            self.name, self.kind, self.shape, self.numel = name, kind, shape, numel
+    cfg = SegConfig(depth=50, pyramid="psp")
+    info = []
+    for s in build_specs(cfg):
+        info.append(PI(s.name + "/weights", "weights", (s.co, s.k, s.k, s.ci), s.co * s.k * s.k * s.ci))
+        info.append(PI(s.name + "/BatchNorm/gamma", "gamma", (s.co,), s.co))
+    ours = init_params(info, seed=7)
+    ref = oracle_init(cfg, seed=7)
+    for k in ours:
+        np.testing.assert_allclose(ours[k].reshape(-1), ref[k].reshape(-1).astype(np.float32))

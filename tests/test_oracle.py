@@ -1,0 +1,135 @@
+"""CPU tests: the oracle against the reference's own golden vectors (tests/golden) and
+against known answers of the TF 1.12 semantics it restates."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import tfseg
+from oracle.tfseg import (CITYSCAPES, OracleNet, SegConfig, build_specs, eval_metrics,
+                          init_params, resize_bilinear_ac, resize_tables, resnet_units, same_pads,
+                          weighted_loss, xent)
+
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "reference_fixtures.npz"))
+
+
+# ---------------------------------------------------------------- reference golden vectors
+@pytest.mark.parametrize("case", range(8))
+def test_bbox_rasterisation_matches_reference(case):
+    from input_pipelines.weak_labels import generate_bbox_rla
+    cids = GOLD[f"bbox{case}_cids"]
+    coords = GOLD[f"bbox{case}_coords"]
+    keep = cids >= 0  # unknown mids are ignored by the reference
+    got = generate_bbox_rla(cids[keep], coords[keep], tuple(GOLD[f"bbox{case}_size"]))
+    exp = GOLD[f"bbox{case}_rla"]
+    np.testing.assert_allclose(got, exp, rtol=0, atol=1e-7)
+    # the reference's own assertion (input_subset_bboxes_v2_test.py:40-43)
+    assert np.all(np.abs(got.sum(-1) - 1.0) < 1e-3)
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_tag_labels_match_reference(case):
+    from input_pipelines.weak_labels import generate_tag_rla
+    got = generate_tag_rla(list(GOLD[f"tag{case}_cids"]))
+    np.testing.assert_allclose(got, GOLD[f"tag{case}_rla"], atol=1e-7)
+    assert abs(got.sum() - 1.0) < 1e-2  # input_subset_image_labels_test.py:41-43
+
+
+@pytest.mark.parametrize("ds", ["cityscapes", "vistas"])
+def test_replacevoids_matches_reference(ds):
+    from utils.utils import _replacevoids
+    assert _replacevoids(list(GOLD[f"replacevoids_{ds}_in"])) == list(GOLD[f"replacevoids_{ds}_out"])
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_eval_metrics_match_reference(case):
+    cm = GOLD[f"cm{case}"]
+    glob, macc, miou, _, _ = eval_metrics(cm)
+    np.testing.assert_allclose([glob, macc, miou], GOLD[f"cm{case}_metrics"], atol=0.0051)
+    from utils.utils import metrics_from_confusion_matrix
+    g2, m2, i2, _, _ = metrics_from_confusion_matrix(cm)
+    np.testing.assert_allclose([g2, m2, i2], [glob, macc, miou], rtol=1e-12)
+
+
+# ---------------------------------------------------------------- TF semantics known answers
+def test_same_padding_and_maxpool_geometry():
+    assert same_pads(512, 3, 2) == (0, 1)      # SAME max-pool: 0 before, 1 after (even size)
+    assert same_pads(128, 3, 1, 4) == (4, 4)   # dilated SAME pad = rate
+    x = torch.arange(2 * 1 * 6 * 6, dtype=torch.float64).reshape(2, 1, 6, 6)
+    y = tfseg.maxpool_same_3x3s2(x)
+    assert y.shape == (2, 1, 3, 3)
+    assert float(y[0, 0, 0, 0]) == float(x[0, 0, 2, 2])   # window rows/cols 0..2 (no front pad)
+    assert float(y[0, 0, 2, 2]) == float(x[0, 0, 5, 5])   # last window clipped by the back pad
+
+
+def test_resize_align_corners_matches_torch():
+    x = torch.randn(2, 5, 7, 9, dtype=torch.float64)
+    ours = resize_bilinear_ac(x, 25, 33)
+    ref = F.interpolate(x, size=(25, 33), mode="bilinear", align_corners=True)
+    assert torch.allclose(ours, ref, atol=1e-5)
+    lo, hi, lerp = resize_tables(16, 128)
+    assert lo[0] == 0 and lerp[0] == 0 and hi[-1] == 15 and lo[-1] in (14, 15)
+
+
+def test_xent_known_answers():
+    logits = torch.zeros(3, 7, 2, 2, dtype=torch.float64, requires_grad=True)
+    y = torch.zeros(3, 7, 2, 2, dtype=torch.float64)
+    y[:, 2] = 1.0
+    loss = xent(logits, y)
+    assert torch.allclose(loss, torch.full_like(loss, math.log(7)))
+    loss.sum().backward()
+    exp = torch.full_like(logits, 1 / 7) - y           # backprop = softmax - labels
+    assert torch.allclose(logits.grad, exp)
+
+
+def test_weighted_loss_safe_division():
+    raw = torch.rand(4, 5, dtype=torch.float64)
+    val, n = weighted_loss(raw, torch.zeros_like(raw))
+    assert float(val) == 0.0 and n == 0
+    w = torch.zeros_like(raw)
+    w[0, :2] = 1.0
+    val, n = weighted_loss(raw, w)
+    assert n == 2 and abs(float(val) - float(raw[0, :2].mean())) < 1e-12
+
+
+def test_unit_schedule_output_stride_8():
+    u = resnet_units(50, 8)
+    assert len(u) == 16 and len(resnet_units(101, 8)) == 33
+    # block1: stride on its last unit; block2 at rate 1; block3 rate 2; block4 rate 4
+    assert [x[4] for x in u[:3]] == [1, 1, 2]
+    assert all(x[4] == 1 for x in u[3:])
+    assert [x[5] for x in u[3:7]] == [1, 1, 1, 1]
+    assert all(x[5] == 2 for x in u[7:13]) and all(x[5] == 4 for x in u[13:])
+
+
+def test_parameter_counts():
+    tot50 = sum(s.co * s.k * s.k * s.ci for s in build_specs(SegConfig(depth=50, pyramid="none")))
+    assert abs(tot50 - 26.15e6) < 0.01e6   # SURVEY §2b (encoder + heads)
+    tot101 = sum(s.co * s.k * s.k * s.ci for s in build_specs(SegConfig(depth=101, pyramid="none")))
+    assert abs(tot101 - 45.09e6) < 0.01e6
+
+
+def test_all_void_labels_give_zero_l1_loss():
+    cfg = SegConfig(height=32, width=32, nb_pp=1, pyramid="none")
+    net = OracleNet(cfg, init_params(cfg, seed=1))
+    low = net.forward(torch.zeros(1, 32, 32, 3, dtype=torch.float64))
+    lab = np.full((1, 32, 32), 19, dtype=np.int64)       # cityscapes void
+    L = net.losses(low, lab)
+    assert float(L["l1_segmentation"]) == 0.0 and L["counts"][0] == 0
+    assert float(L["l2_vehicle_segmentation"]) == 0.0 and L["counts"][1] == 0
+
+
+def test_weak_weights_follow_l1_decision():
+    """A weak pixel contributes to the vehicle loss iff l1 decides 'vehicle' (:233-237)."""
+    cfg = SegConfig(height=32, width=32, nb_pp=0, nb_pb=1, pyramid="none")
+    net = OracleNet(cfg, init_params(cfg, seed=2))
+    low = net.forward(torch.zeros(1, 32, 32, 3, dtype=torch.float64))
+    soft = np.zeros((1, 32, 32, 15))
+    soft[..., 2] = 1.0                                    # 'car' box everywhere
+    L = net.losses(low, np.zeros((0, 32, 32), np.int64), bbox_soft=soft)
+    dec = L["decisions"]["l1_logits"].numpy()
+    assert L["counts"][1] == int((dec == CITYSCAPES["cid_l1_vehicle"]).sum())
+    assert L["counts"][2] == 0                            # car boxes are void for the human head
