@@ -100,6 +100,12 @@ int seg_outputs(seg_ctx* ctx, const float** losses, const float** reg,
 int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions, int64_t n,
                   int num_classes, int32_t* cm, void* stream);
 
+/* internal tensors for parity tests: "logits", "grad_un", "dzscale", "feat", "dfeat",
+ * "head<h>_out", "head<h>_dout", "conv<i>_x" (input of the last forward), "conv<i>_y",
+ * "conv<i>_dy" (i = creation index).
+ * dims = N, H, W, C; ld = pixel stride; dtype = SEG_DTYPE_* of the storage */
+int seg_debug_tensor(seg_ctx* ctx, const char* name, void** ptr, int* dims, int* ld, int* dtype);
+
 /* kernel-time profiling of conv classes (0 fwd, 1 dgrad, 2 wgrad) ---------------------- */
 int seg_profile(seg_ctx* ctx, int enable);
 int seg_profile_read(seg_ctx* ctx, int cls, double* ms_total, double* gflop_total,

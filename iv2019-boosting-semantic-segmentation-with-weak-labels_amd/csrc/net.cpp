@@ -50,6 +50,7 @@ struct ConvL {
   void* w_lp = nullptr;           // compute-dtype weights [co][k][k][ci]
   void* wt_lp = nullptr;          // flipped transpose [ci][k][k][co] (dgrad)
   bool need_dgrad = true;
+  Act x;                          // input of the last forward (not owned)
   Act y, dy;                      // conv output and its gradient
   BnState st{};
   float* stats_part = nullptr;    // [mtiles][co][2]
@@ -362,6 +363,7 @@ int prof_end(seg_ctx* c, hipStream_t s, int slot) {
 int conv_forward(Step& S, int li, const Act& x) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
+  L.x = x;
   ConvArgs a{};
   a.x = x.p; a.N = x.N; a.H = x.H; a.W = x.W; a.C = x.C; a.ldx = x.ld;
   a.w = L.w_lp; a.ldw = L.k * L.k * L.ci;
@@ -1025,6 +1027,40 @@ int seg_confusion(seg_ctx* c, const int32_t* labels, const int32_t* decisions, i
   hipError_t e = hipMemsetAsync(cm, 0, (size_t)num_classes * num_classes * 4, s);
   if (e == hipSuccess) e = launch_confusion(labels, decisions, n, num_classes, cm, s);
   if (e != hipSuccess) return hip_fail(c, e, "seg_confusion");
+  return 0;
+}
+
+int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* ld, int* dtype) {
+  if (!c || !name) return set_err(c ? &c->err : nullptr, -EINVAL, "null argument");
+  std::string n(name);
+  Act a;
+  int dt = c->dt == SEG_BF16 ? SEG_DTYPE_BF16 : SEG_DTYPE_F32;
+  if (n == "logits") { a = c->logits; dt = SEG_DTYPE_F32; }
+  else if (n == "grad_un") { a = c->logits; a.p = c->grad_un; dt = SEG_DTYPE_F32; }
+  else if (n == "dzscale") { a.p = c->dzscale; a.N = a.H = a.W = 1; a.C = a.ld = c->ldl; dt = SEG_DTYPE_F32; }
+  else if (n == "feat") a = c->feat;
+  else if (n == "dfeat") a = c->dfeat;
+  else if (n.rfind("head", 0) == 0 && n.size() > 5) {
+    int h = n[4] - '0';
+    if (h < 0 || h > 2) return set_err(&c->err, -EINVAL, "bad head");
+    if (n.substr(5) == "_out") a = c->heads[h].out;
+    else if (n.substr(5) == "_dout") a = c->heads[h].dout;
+    else return set_err(&c->err, -EINVAL, "unknown tensor %s", name);
+  } else if (n.rfind("conv", 0) == 0) {
+    size_t us = n.find('_');
+    int i = atoi(n.substr(4, us - 4).c_str());
+    if (i < 0 || i >= (int)c->convs.size() || us == std::string::npos) return set_err(&c->err, -EINVAL, "bad conv");
+    if (n.substr(us) == "_x") a = c->convs[i].x;
+    else if (n.substr(us) == "_y") a = c->convs[i].y;
+    else if (n.substr(us) == "_dy") a = c->convs[i].dy;
+    else return set_err(&c->err, -EINVAL, "unknown tensor %s", name);
+  } else {
+    return set_err(&c->err, -EINVAL, "unknown tensor %s", name);
+  }
+  if (ptr) *ptr = a.p;
+  if (dims) { dims[0] = a.N; dims[1] = a.H; dims[2] = a.W; dims[3] = a.C; }
+  if (ld) *ld = a.ld;
+  if (dtype) *dtype = dt;
   return 0;
 }
 

@@ -20,7 +20,8 @@ LIB_PATH = os.path.join(_HERE, "libseg_hip.so")
 EXPORTED_SYMBOLS = [
     "seg_create", "seg_destroy", "seg_last_error", "seg_sizes", "seg_bind_buffers",
     "seg_param_count", "seg_param_info", "seg_param_shape", "seg_params_updated", "seg_forward", "seg_loss",
-    "seg_backward", "seg_apply_update", "seg_outputs", "seg_confusion", "seg_profile",
+    "seg_backward", "seg_apply_update", "seg_outputs", "seg_confusion", "seg_debug_tensor",
+    "seg_profile",
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_dgrad", "seg_op_conv_wgrad",
 ]
 
@@ -69,6 +70,8 @@ def _load():
         "seg_outputs": (ip, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
                              ctypes.POINTER(ip), ctypes.POINTER(ip), ctypes.POINTER(ip)]),
         "seg_confusion": (ip, [vp, vp, vp, i64, ip, vp, vp]),
+        "seg_debug_tensor": (ip, [vp, ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(ip),
+                                  ctypes.POINTER(ip), ctypes.POINTER(ip)]),
         "seg_profile": (ip, [vp, ip]),
         "seg_profile_read": (ip, [vp, ip, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
@@ -221,6 +224,22 @@ class SegContext:
         check(LIB.seg_confusion(self.h, _ptr(labels), _ptr(decisions), labels.numel(),
                                 num_classes, _ptr(out), _stream(stream)), self.h)
 
+    def debug_tensor(self, name: str):
+        """Host copy (float32, [N,H,W,C]) of an internal tensor (parity tests only)."""
+        import torch
+        ptr = ctypes.c_void_p()
+        dims = (ctypes.c_int * 4)()
+        ld, dt = ctypes.c_int(), ctypes.c_int()
+        check(LIB.seg_debug_tensor(self.h, name.encode(), ctypes.byref(ptr), dims, ctypes.byref(ld),
+                                   ctypes.byref(dt)), self.h)
+        n, hh, ww, c = list(dims)
+        torch.cuda.synchronize()
+        if dt.value == 0:
+            t = _wrap(ptr.value, (n * hh * ww, ld.value), self.device)
+        else:
+            t = _wrap_u16(ptr.value, (n * hh * ww, ld.value), self.device)
+        return t[:, :c].float().cpu().numpy().reshape(n, hh, ww, c)
+
     def profile(self, enable: bool):
         check(LIB.seg_profile(self.h, int(enable)), self.h)
 
@@ -243,6 +262,18 @@ class SegContext:
             self.close()
         except Exception:
             pass
+
+
+def _wrap_u16(ptr: int, shape: Tuple[int, ...], device):
+    """Zero-copy view of a bf16 device buffer (reinterpreted from int16)."""
+    import torch
+
+    class _CAI:
+        pass
+    o = _CAI()
+    o.__cuda_array_interface__ = {"shape": shape, "typestr": "<i2", "data": (ptr, False),
+                                  "version": 3, "strides": None}
+    return torch.as_tensor(o, device=device).view(torch.bfloat16)
 
 
 def _wrap(ptr: int, shape: Tuple[int, ...], device):
