@@ -1,0 +1,167 @@
+"""Training-throughput benchmark of the MI355X path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+
+Workload (BASELINE config C2, the metric's single-GPU configuration): ResNet-50 dilated
+(output stride 8) + PSP pyramid (the reference's live pyramid; ASPP exists only as a
+comment in the reference), 1024x2048 crops, 4 per-pixel-labelled images per GPU, bf16
+storage with fp32 accumulation, synthetic seeded data resident in HBM. One step = forward +
+fused multi-loss head + backward + gradient all-reduce (RCCL, N>1) + fused SGDM/L2/BN
+moving-average update. Weak scaling: 4 images per GPU at every N.
+
+Prints ONE JSON line (rank 0) with the metric, a roofline object for the dominant kernel
+class (HIP-event timed inside the timed region) and the CPU baseline (the oracle — a
+PyTorch-CPU fp32 restatement of the reference semantics — timed on this host's cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd")
+sys.path[:0] = [REPO, PKG]
+
+H, W, NB = 1024, 2048, 4
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+CLS_NAMES = {0: "conv_nt_kernel (forward implicit GEMM)", 1: "conv_nt_kernel (data-gradient)",
+             2: "conv_wgrad_kernel (weight-gradient, split-K)"}
+
+
+def cpu_baseline(threads):
+    """Oracle (PyTorch-CPU fp32 restatement of the TF semantics) on a bounded sample:
+    one 1024x2048 image, one full training step, after a 256x512 warm-up."""
+    import numpy as np
+    import torch
+    from input_pipelines.synthetic import batch
+    from oracle.tfseg import OracleNet, SegConfig, init_params
+    torch.set_num_threads(threads)
+    warm = SegConfig(height=256, width=512, nb_pp=1, pyramid="psp")
+    d = batch(1, 1, 0, 0, 256, 512)
+    OracleNet(warm, init_params(warm), dtype=torch.float32).train_step(d["images"], d["px"])
+    cfg = SegConfig(height=H, width=W, nb_pp=1, pyramid="psp")
+    net = OracleNet(cfg, init_params(cfg), dtype=torch.float32)
+    d = batch(2, 1, 0, 0, H, W)
+    t = time.perf_counter()
+    net.train_step(d["images"], d["px"])
+    dt = time.perf_counter() - t
+    return {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": "1 image 1024x2048, 1 full step (fwd+loss+bwd+SGDM), R50+PSP, fp32, "
+                      f"oracle/tfseg.py on {threads} host threads ({dt:.1f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from estimator.define_estimator_hierarchical import allreduce_grads
+    from input_pipelines.synthetic import batch
+    from models.initializers import init_params
+    from seg_hip import SegContext
+
+    ctx = SegContext(depth=50, pyramid="psp", height=H, width=W, nb_pp=NB, dtype=args.dtype,
+                     device=local)
+    ctx.load_params(init_params(ctx.param_info, seed=0))
+    data = batch(1000 + rank, NB, 0, 0, H, W)
+    img = torch.as_tensor(data["images"]).to(dev)
+    px = torch.as_tensor(data["px"]).to(dev)
+
+    def step():
+        ctx.forward(img)
+        ctx.loss(px)
+        ctx.backward()
+        scale = allreduce_grads(ctx)
+        ctx.apply_update(0.01, 0.9, 0.0, scale)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not args.no_profile:
+        ctx.profile(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    losses, _, _ = ctx.outputs()
+    lv = losses.cpu().numpy()
+    if not np.all(np.isfinite(lv)):
+        raise RuntimeError(f"non-finite losses {lv}")
+
+    roofline = None
+    if not args.no_profile:
+        cls = {c: ctx.profile_read(c) for c in (0, 1, 2)}
+        dom = max(cls, key=lambda c: cls[c]["ms"])
+        r = cls[dom]
+        peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+        achieved = r["gflop"] / r["ms"]  # GFLOP/ms == TFLOP/s
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                    "kernel": CLS_NAMES[dom],
+                    "launches": r["launches"],
+                    "avg_launch_ms": round(r["ms"] / max(r["launches"], 1), 4),
+                    "share_of_step": round(r["ms"] / (elapsed * 1e3), 3),
+                    "classes_ms_per_step": {CLS_NAMES[c]: round(cls[c]["ms"] / args.steps, 2)
+                                            for c in cls},
+                    "max_layer": r["max_layer"]}
+        ctx.profile(False)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(threads=min(16, os.cpu_count() or 1))
+
+    if rank == 0:
+        value = world * NB * args.steps / elapsed
+        out = {"metric": "training images/sec at 1024x2048 bf16, 1/2/4/8 MI355X + mIoU vs ref",
+               "value": round(value, 3), "unit": "images/sec", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(elapsed * 1e3 / args.steps, 2),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": args.dtype, "data": "synthetic (seeded; random-init weights)",
+               "config": {"workload": "C2: ResNet-50 dilated OS8 + PSP, 1024x2048, per-pixel "
+                                      "CE multi-loss head, fwd+loss+bwd+allreduce+SGDM",
+                          "global_batch": world * NB, "per_gpu_batch": NB,
+                          "image": [H, W], "parallelism": f"dp{world}"},
+               "losses_last_step": [round(float(x), 5) for x in lv[:4]],
+               "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

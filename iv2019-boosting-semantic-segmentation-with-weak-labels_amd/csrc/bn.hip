@@ -188,19 +188,38 @@ __global__ void bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
 }
 
+// block = 8 channels (fast) x 32 row-block lanes; fixed-order float sums, then an LDS tree
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int rb, long M, int C,
                                        BnState st, float* dgamma, float* dbeta) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int k = 0; k < rb; ++k) {
-    s1 += part[2 * ((size_t)k * C + c)];
-    s2 += part[2 * ((size_t)k * C + c) + 1];
+  __shared__ float sh[2][32][9];
+  const int cl = threadIdx.x & 7, lane = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  float s1 = 0.f, s2 = 0.f;
+  if (c < C) {
+    for (int k = lane; k < rb; k += 32) {
+      const float2 v = *(const float2*)(part + 2 * ((size_t)k * C + c));
+      s1 += v.x;
+      s2 += v.y;
+    }
   }
-  st.sdy[c] = (float)(s1 / (double)M);
-  st.sdyx[c] = (float)(s2 / (double)M);
-  if (dgamma) dgamma[c] = (float)s2;
-  if (dbeta) dbeta[c] = (float)s1;
+  sh[0][lane][cl] = s1;
+  sh[1][lane][cl] = s2;
+  __syncthreads();
+  for (int st2 = 16; st2 > 0; st2 >>= 1) {
+    if (lane < st2) {
+      sh[0][lane][cl] += sh[0][lane + st2][cl];
+      sh[1][lane][cl] += sh[1][lane + st2][cl];
+    }
+    __syncthreads();
+  }
+  if (lane == 0 && c < C) {
+    s1 = sh[0][0][cl];
+    s2 = sh[1][0][cl];
+    st.sdy[c] = s1 / (float)M;
+    st.sdyx[c] = s2 / (float)M;
+    if (dgamma) dgamma[c] = s2;
+    if (dbeta) dbeta[c] = s1;
+  }
 }
 
 template <typename T, typename TZ, int VEC>
@@ -336,8 +355,8 @@ hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipSt
 
 hipError_t launch_bn_bwd_finalize(const float* part, int rb, long M, int C, BnState st,
                                   float* dgamma, float* dbeta, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, s, part, rb, M, C,
-                     st, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 8)), dim3(256), 0, s, part, rb, M,
+                     C, st, dgamma, dbeta);
   return hipGetLastError();
 }
 

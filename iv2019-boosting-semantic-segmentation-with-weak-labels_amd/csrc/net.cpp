@@ -104,6 +104,7 @@ struct seg_ctx {
   Act img;                        // compute-dtype images
   int stem = -1;
   Act z0, dz0, p0, dp0;
+  uint8_t* pool_arg = nullptr;    // max-pool first-max window index per output element
   int pool_ph = 0, pool_pw = 0;
   std::vector<Unit> units;
   int dfd = -1;
@@ -624,6 +625,7 @@ int build(seg_ctx* c) {
     int th = std::max((Ho - 1) * 2 + 3 - st.Ho, 0), tw = std::max((Wo - 1) * 2 + 3 - st.Wo, 0);
     c->pool_ph = th / 2; c->pool_pw = tw / 2;
     if (int r = alloc_act(c, c->p0, N, Ho, Wo, 64)) return r;
+    if (int r = dalloc(c, &c->pool_arg, (size_t)N * Ho * Wo * 64)) return r;
     if (int r = alloc_act(c, c->dp0, N, Ho, Wo, 64)) return r;
   }
   Act x = c->p0;
@@ -770,7 +772,8 @@ int forward(Step& S, const float* images) {
   if (int r = conv_forward(S, c->stem, c->img)) return r;
   if (int r = bn_apply(S, c->stem, c->z0, 0)) return r;
   HIPCALL(c, launch_maxpool_fwd(S.dt, c->z0.p, c->z0.N, c->z0.H, c->z0.W, 64, c->z0.ld, c->p0.p,
-                                c->p0.H, c->p0.W, c->p0.ld, c->pool_ph, c->pool_pw, S.s));
+                                c->p0.H, c->p0.W, c->p0.ld, c->pool_ph, c->pool_pw, c->pool_arg,
+                                S.s));
   for (auto& u : c->units)
     if (int r = unit_forward(S, u)) return r;
   if (int r = conv_forward(S, c->dfd, c->units.back().out)) return r;
@@ -840,7 +843,7 @@ int backward(Step& S) {
     const Act& dx = i == 0 ? c->dp0 : c->units[i - 1].dout;
     if (int r = unit_backward(S, c->units[i], dx, false)) return r;
   }
-  HIPCALL(c, launch_maxpool_bwd(S.dt, c->z0.p, c->z0.N, c->z0.H, c->z0.W, 64, c->z0.ld, c->dp0.p,
+  HIPCALL(c, launch_maxpool_bwd(S.dt, c->pool_arg, c->z0.N, c->z0.H, c->z0.W, 64, c->dp0.p,
                                 c->dp0.H, c->dp0.W, c->dp0.ld, c->dz0.p, c->dz0.ld, c->pool_ph,
                                 c->pool_pw, S.s));
   if (int r = bn_backward(S, c->stem, c->dz0, 0, &c->z0, nullptr)) return r;

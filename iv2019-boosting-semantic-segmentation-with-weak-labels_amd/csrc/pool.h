@@ -21,10 +21,12 @@ struct GridSpec {
   const float* coltab;            // device [total_rcells][H]: weight of row h for cell
 };
 
+// max pool 3x3/2 (TF SAME): also writes the first-max window index (0..8) per output
+// element to arg[N*Ho*Wo][C] (bytes); the backward gathers through it
 hipError_t launch_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
-                              void* y, int Ho, int Wo, int ldy, int pad_h, int pad_w,
+                              void* y, int Ho, int Wo, int ldy, int pad_h, int pad_w, void* arg,
                               hipStream_t s);
-hipError_t launch_maxpool_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+hipError_t launch_maxpool_bwd(int dtype, const void* arg, int N, int H, int W, int C,
                               const void* dy, int Ho, int Wo, int lddy, void* dx, int lddx,
                               int pad_h, int pad_w, hipStream_t s);
 // dx[n][ho*s][wo*s][c] += g[n][ho][wo][c]

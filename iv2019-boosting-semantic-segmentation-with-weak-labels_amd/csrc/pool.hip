@@ -12,7 +12,8 @@ inline int grid_for(long items) {
 // ---- max pool 3x3 stride 2, TF SAME padding (pads are -inf, i.e. ignored) ---------------
 template <typename T>
 __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W, int C, int ldx,
-                                   T* __restrict__ y, int Ho, int Wo, int ldy, int ph, int pw) {
+                                   T* __restrict__ y, int Ho, int Wo, int ldy, int ph, int pw,
+                                   uint8_t* __restrict__ arg) {
   const int cg_n = C / 8;
   const long total = (long)N * Ho * Wo * cg_n;
   for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
@@ -24,8 +25,9 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W,
     int ho = (int)(t % Ho);
     int n = (int)(t / Ho);
     float mx[8];
+    uint32_t am[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
+    for (int e = 0; e < 8; ++e) { mx[e] = -INFINITY; am[e] = 255; }
     for (int dh = 0; dh < 3; ++dh) {
       int hi = ho * 2 - ph + dh;
       if (hi < 0 || hi >= H) continue;
@@ -35,16 +37,22 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W,
         float v[8];
         Vec8<T>::load(x + ((size_t)((long)n * H + hi) * W + wi) * ldx + cg * 8, v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) mx[e] = v[e] > mx[e] ? v[e] : mx[e];
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > mx[e]) { mx[e] = v[e]; am[e] = dh * 3 + dw; }  // first max wins
       }
     }
-    Vec8<T>::store(y + ((size_t)((long)n * Ho + ho) * Wo + wo) * ldy + cg * 8, mx);
+    Vec8<T>::store(y + p * ldy + cg * 8, mx);
+    uint2 packed;
+    packed.x = am[0] | (am[1] << 8) | (am[2] << 16) | (am[3] << 24);
+    packed.y = am[4] | (am[5] << 8) | (am[6] << 16) | (am[7] << 24);
+    *(uint2*)(arg + (size_t)p * C + cg * 8) = packed;
   }
 }
 
-// gather form: each input pixel sums the gradients of the windows whose first max it is
+// gather form: each input pixel sums the gradients of the (<= 4) windows whose stored first
+// max (forward argmax byte) is this pixel — no atomics, no recomputation
 template <typename T>
-__global__ void maxpool_bwd_kernel(const T* __restrict__ x, int N, int H, int W, int C, int ldx,
+__global__ void maxpool_bwd_kernel(const uint8_t* __restrict__ arg, int N, int H, int W, int C,
                                    const T* __restrict__ dy, int Ho, int Wo, int lddy,
                                    T* __restrict__ dx, int lddx, int ph, int pw) {
   const int cg_n = C / 8;
@@ -68,30 +76,20 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ x, int N, int H, int W,
     int wo_hi = (wi + pw) >> 1;
     for (int ho = ho_lo; ho <= ho_hi && ho < Ho; ++ho) {
       for (int wo = wo_lo; wo <= wo_hi && wo < Wo; ++wo) {
-        // first max of window (ho, wo) per channel
-        float mx[8];
-        int arg[8];
+        const size_t q = (size_t)((long)n * Ho + ho) * Wo + wo;
+        const uint2 a = *(const uint2*)(arg + q * C + cg * 8);
+        const uint32_t me = (uint32_t)((hi - (ho * 2 - ph)) * 3 + (wi - (wo * 2 - pw)));
+        uint32_t b[8] = {a.x & 255, (a.x >> 8) & 255, (a.x >> 16) & 255, a.x >> 24,
+                         a.y & 255, (a.y >> 8) & 255, (a.y >> 16) & 255, a.y >> 24};
+        bool any = false;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { mx[e] = -INFINITY; arg[e] = -1; }
-        for (int dh = 0; dh < 3; ++dh) {
-          int h2 = ho * 2 - ph + dh;
-          if (h2 < 0 || h2 >= H) continue;
-          for (int dw = 0; dw < 3; ++dw) {
-            int w2 = wo * 2 - pw + dw;
-            if (w2 < 0 || w2 >= W) continue;
-            float v[8];
-            Vec8<T>::load(x + ((size_t)((long)n * H + h2) * W + w2) * ldx + cg * 8, v);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (v[e] > mx[e]) { mx[e] = v[e]; arg[e] = dh * 3 + dw; }
-          }
-        }
-        const int me = (hi - (ho * 2 - ph)) * 3 + (wi - (wo * 2 - pw));
+        for (int e = 0; e < 8; ++e) any |= b[e] == me;
+        if (!any) continue;
         float g[8];
-        Vec8<T>::load(dy + ((size_t)((long)n * Ho + ho) * Wo + wo) * lddy + cg * 8, g);
+        Vec8<T>::load(dy + q * lddy + cg * 8, g);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (arg[e] == me) acc[e] += g[e];
+          if (b[e] == me) acc[e] += g[e];
       }
     }
     Vec8<T>::store(dx + ((size_t)((long)n * H + hi) * W + wi) * lddx + cg * 8, acc);
@@ -263,30 +261,30 @@ __global__ void psp_input_bwd_kernel(const T* __restrict__ dcat, int ldcat, Grid
 }  // namespace
 
 hipError_t launch_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
-                              void* y, int Ho, int Wo, int ldy, int pad_h, int pad_w,
+                              void* y, int Ho, int Wo, int ldy, int pad_h, int pad_w, void* arg,
                               hipStream_t s) {
   if (C % 8 || ldx % 8 || ldy % 8) return hipErrorInvalidValue;
   dim3 g(grid_for((long)N * Ho * Wo * C / 8));
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, N, H, W, C,
-                       ldx, (bf16_t*)y, Ho, Wo, ldy, pad_h, pad_w);
+                       ldx, (bf16_t*)y, Ho, Wo, ldy, pad_h, pad_w, (uint8_t*)arg);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, dim3(256), 0, s, (const float*)x, N, H, W, C,
-                       ldx, (float*)y, Ho, Wo, ldy, pad_h, pad_w);
+                       ldx, (float*)y, Ho, Wo, ldy, pad_h, pad_w, (uint8_t*)arg);
   return hipGetLastError();
 }
 
-hipError_t launch_maxpool_bwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
+hipError_t launch_maxpool_bwd(int dtype, const void* arg, int N, int H, int W, int C,
                               const void* dy, int Ho, int Wo, int lddy, void* dx, int lddx,
                               int pad_h, int pad_w, hipStream_t s) {
-  if (C % 8 || ldx % 8 || lddy % 8 || lddx % 8) return hipErrorInvalidValue;
+  if (C % 8 || lddy % 8 || lddx % 8) return hipErrorInvalidValue;
   dim3 g(grid_for((long)N * H * W * C / 8));
   if (dtype == SEG_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, N, H, W, C,
-                       ldx, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, pad_h, pad_w);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, N, H, W,
+                       C, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, pad_h, pad_w);
   else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, dim3(256), 0, s, (const float*)x, N, H, W, C,
-                       ldx, (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, pad_h, pad_w);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, dim3(256), 0, s, (const uint8_t*)arg, N, H, W,
+                       C, (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, pad_h, pad_w);
   return hipGetLastError();
 }
 
