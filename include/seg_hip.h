@@ -110,11 +110,15 @@ int seg_debug_tensor(seg_ctx* ctx, const char* name, void** ptr, int* dims, int*
 int seg_profile(seg_ctx* ctx, int enable);
 int seg_profile_read(seg_ctx* ctx, int cls, double* ms_total, double* gflop_total,
                      int64_t* launches, double* ms_max_layer, char* layer_name, int name_len);
+/* one text line per recorded launch: cls name ci co k rate Ho Wo gflop ms */
+int seg_profile_dump(seg_ctx* ctx, char* buf, int len);
 
 /* single-op entry points (parity tests of individual kernels) -------------------------- */
 int seg_op_conv_fwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
                     const void* w, int Co, int k, int stride, int rate, int explicit_pad,
                     void* y, int ldy, float* stats, void* stream);
+/* rows per BN-statistics partial written by seg_op_conv_fwd for this shape (128 or 256) */
+int seg_op_conv_stat_rows(int dtype, int C, int ldx, int Co, int ldy);
 int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
                       const void* w, int Ci, int k, int stride, int rate, int explicit_pad,
                       int H, int W, void* dx, int lddx, void* stream);

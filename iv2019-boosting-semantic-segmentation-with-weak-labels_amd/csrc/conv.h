@@ -46,4 +46,11 @@ hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride
                                 float* out, int accumulate, hipStream_t s);
 hipError_t launch_weight_flip_transpose(int dtype, const void* w, void* wt, int co, int kh, int kw,
                                         int ci, hipStream_t s);
-int conv_nt_mtiles(long M);  // rows per BN-stat partial = 128
+int conv_nt_mtiles(long M);  // upper bound on BN-stat partial tiles (128-row tiles)
+// rows per BN-stat partial tile of the kernel launch_conv_nt will pick (128 or 256)
+int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a);
+bool conv_nt_v2_ok(const ConvArgs& a);
+hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s);
+bool conv_wgrad_v2_ok(const WgradArgs& a);
+hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s);
+void conv_wgrad_v2_tile(int Co, int Ncol, int* bm, int* bn);

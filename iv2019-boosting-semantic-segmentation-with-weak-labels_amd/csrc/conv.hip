@@ -586,7 +586,12 @@ hipError_t wg_dispatch(const WgradArgs& a, hipStream_t s) {
 
 int conv_nt_mtiles(long M) { return ceil_div(M, 128); }
 
+int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a) {
+  return (dtype == SEG_BF16 && !out_f32 && conv_nt_v2_ok(a)) ? 256 : 128;
+}
+
 hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t s) {
+  if (dtype == SEG_BF16 && !out_f32 && conv_nt_v2_ok(a)) return launch_conv_nt_v2(a, s);
   if (dtype == SEG_BF16) {
     if (out_f32) return nt_dispatch<bf16_t, float>(a, s);
     return nt_dispatch<bf16_t, bf16_t>(a, s);
@@ -595,6 +600,7 @@ hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t
 }
 
 hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s) {
+  if (dtype == SEG_BF16 && conv_wgrad_v2_ok(a)) return launch_conv_wgrad_v2(a, s);
   if (dtype == SEG_BF16) return wg_dispatch<bf16_t>(a, s);
   return wg_dispatch<float>(a, s);
 }

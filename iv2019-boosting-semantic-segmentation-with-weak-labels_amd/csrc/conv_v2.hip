@@ -1,0 +1,584 @@
+// bf16 implicit-GEMM convolution, forward + data-gradient ("NT"), v2 structure for gfx950:
+//
+//  * 512 threads = 8 waves, block tile BM=256 pixels x BN output channels, K-step 64 bf16;
+//  * operands staged HBM -> LDS with LDS-DMA (global_load_lds_dwordx4, no VGPR staging),
+//    STAGES-deep ring, loads of the next K-steps in flight across the barrier (counted
+//    s_waitcnt vmcnt + raw s_barrier: __syncthreads would drain the DMA);
+//  * the implicit-GEMM gather is per-lane SOURCE addressing (TF SAME / explicit padding,
+//    dilation, forward stride, transposed-conv stride for dgrad); out-of-bounds taps read
+//    from a 16-byte zero buffer, so the LDS image is always written whole;
+//  * XOR-swizzled 128-byte LDS rows (chunk ^ ((row>>1)&7)) applied on the source address,
+//    conflict-free ds_read_b128 fragment reads, v_mfma_f32_16x16x32_bf16;
+//  * XCD-aware block -> tile map (blocks sharing an A panel land on one XCD's L2);
+//  * epilogue staged through LDS in fp32 column chunks: optional residual adds, one 16-byte
+//    store per 8 outputs, and the per-column BN partial statistics (sum, M2 about the tile
+//    mean) for the fused batch-norm.
+#include "conv.h"
+
+// 16-byte zero source for out-of-bounds (padding) taps of the LDS-DMA gather
+__device__ __attribute__((aligned(64))) bf16_t g_zero16[64];
+
+namespace {
+
+constexpr int V2_THREADS = 512;
+constexpr int BK = 64;     // bf16 elements per K-step (128 B per row)
+
+__device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int TO_F32>
+struct OutT;
+template <> struct OutT<0> { typedef bf16_t T; };
+template <> struct OutT<1> { typedef float T; };
+
+// BM = 256; waves laid out WMW (M) x WNW (N)
+template <int BN, int WMW, int WNW, int STAGES, int ST>
+__global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
+  const bf16_t* zero = g_zero16;
+  constexpr int BM = 256;
+  constexpr int WM = BM / WMW, WN = BN / WNW;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int AI = BM * 8 / V2_THREADS;       // A glds per lane per K-step (4)
+  constexpr int BI = BN * 8 / V2_THREADS;       // B glds per lane per K-step
+  constexpr int LPK = AI + BI;
+  constexpr int STAGE_BYTES = (BM + BN) * 128;
+  constexpr int EPI_COLS = 64;                  // epilogue chunk width (fp32 staging)
+  constexpr int EPI_LD = EPI_COLS + 4;          // padded fp32 row
+  constexpr int LDS_BYTES = STAGES * STAGE_BYTES > BM * EPI_LD * 4 ? STAGES * STAGE_BYTES : BM * EPI_LD * 4;
+  static_assert(WMW * WNW == 8, "8 waves");
+  static_assert(BI >= 1, "BN >= 64");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  (void)LDS_BYTES;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int lr = lane & 15, lq = lane >> 4;
+  const long M = (long)a.N * a.Ho * a.Wo;
+  const int mtiles = (int)((M + BM - 1) / BM);
+  const int ntiles = (a.Co + BN - 1) / BN;
+  // XCD-aware bijective remap: blocks dealt round-robin over 8 XCDs; give each XCD a
+  // contiguous run of tiles (n fastest) so blocks sharing an A panel share an L2
+  const int nwg = mtiles * ntiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const long m0 = (long)mt * BM;
+  const int n0 = nt * BN;
+  const int K = a.KH * a.KW * a.C;
+  const int nk = K / BK;
+  const bf16_t* X = (const bf16_t*)a.x;
+  const bf16_t* Wt = (const bf16_t*)a.w;
+
+  // ---- per-lane A rows (fixed over K): image base and the tap-independent coordinates ----
+  const int pc = lane & 7;        // physical 16-B chunk this lane fills
+  long a_nb[AI];                  // n * H
+  int a_h0[AI], a_w0[AI], a_row[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+    a_row[i] = row;
+    const long m = m0 + row;
+    const bool ok = m < M;
+    const long mm = ok ? m : 0;
+    const int wo = (int)(mm % a.Wo);
+    const long t = mm / a.Wo;
+    const int ho = (int)(t % a.Ho);
+    a_nb[i] = (t / a.Ho) * a.H;
+    a_h0[i] = ok ? ho * a.sf - a.pad_h : -(1 << 28);  // invalid rows never pass the bounds test
+    a_w0[i] = wo * a.sf - a.pad_w;
+  }
+
+  auto issue = [&](int kb, int stage) {
+    const int k0 = kb * BK;
+    const int tap = k0 / a.C;
+    const int c0 = k0 - tap * a.C;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const int dh = kh * a.dil, dw = kw * a.dil;
+    char* sA = smem + stage * STAGE_BYTES;
+    char* sB = sA + BM * 128;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int lc = swz(a_row[i], pc);
+      int hi = a_h0[i] + dh, wi = a_w0[i] + dw;
+      bool ok;
+      if constexpr (ST == 1) {
+        ok = ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
+      } else {  // transposed-conv gather (strided dgrad): source index must divide by ST
+        ok = (hi >= 0) & (wi >= 0) & ((hi % ST) == 0) & ((wi % ST) == 0);
+        hi /= ST;
+        wi /= ST;
+        ok &= (hi < a.H) & (wi < a.W);
+      }
+      const size_t off = ((size_t)(a_nb[i] + hi) * a.W + wi) * a.ldx + c0 + lc * 8;
+      glds16(ok ? (const void*)(X + off) : (const void*)zero, sA + (i * 8 + wave) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = (i * 8 + wave) * 8 + (lane >> 3);
+      const int co = n0 + row;
+      const int lc = swz(row, pc);
+      const bf16_t* src = co < a.Co ? Wt + (size_t)co * a.ldw + k0 + lc * 8 : zero;
+      glds16(src, sB + (i * 8 + wave) * 1024);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int stage) {
+    const char* A = smem + stage * STAGE_BYTES;
+    const char* B = A + BM * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * WM + i * 16 + lr;
+        af[i] = *(const bf16x8_t*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * WN + j * 16 + lr;
+        bfr[j] = *(const bf16x8_t*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // ---- main loop: STAGES-deep LDS ring filled by LDS-DMA ----
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int kb = 0; kb < nk; ++kb) {
+    // K-step kb has landed for this lane once at most (issued later) steps remain in flight
+    if constexpr (STAGES == 3) {
+      if (kb + 1 < nk) wait_vmcnt<LPK>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();   // every lane's DMA for kb landed; stage (kb-1) is free
+    if (kb + STAGES - 1 < nk) issue(kb + STAGES - 1, (kb + STAGES - 1) % STAGES);
+    compute(kb % STAGES);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // ---- epilogue ----
+  const int rows_valid = (int)((M - m0) < BM ? (M - m0) : BM);
+  float* red = (float*)smem;          // [WMW][BN] column partials
+  if (a.stats) {
+    // BN statistics straight from the accumulators (values rounded as stored):
+    // column sums over the wave's rows -> lane groups (shfl) -> the WMW waves (LDS)
+    float cs[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WM + i * 16 + lq * 4 + r;
+          const float x = row < rows_valid ? bf2f(f2bf(acc[i][j][r])) : 0.f;
+          v += x;
+        }
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      cs[j] = v;
+    }
+    if (lq == 0)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + wn * WN + j * 16 + lr] = cs[j];
+    __syncthreads();
+    float mean[FN], tot[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = wn * WN + j * 16 + lr;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
+      tot[j] = t;
+      mean[j] = t / (float)rows_valid;
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WM + i * 16 + lq * 4 + r;
+          const float d = bf2f(f2bf(acc[i][j][r])) - mean[j];
+          v += row < rows_valid ? d * d : 0.f;
+        }
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      cs[j] = v;
+    }
+    __syncthreads();
+    if (lq == 0)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + wn * WN + j * 16 + lr] = cs[j];
+    __syncthreads();
+    if (wm == 0 && lq == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * WN + j * 16 + lr;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
+        if (n0 + c < a.Co)   // one (sum, M2) per 256-row tile (conv_nt_stat_rows)
+          *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = make_float2(tot[j], t);
+      }
+    }
+    __syncthreads();
+  }
+  // coalesced stores: fp32 tile staged through LDS 64 columns at a time, 16 B per lane
+  float* stage = (float*)smem;
+  bf16_t* Y = (bf16_t*)a.y;
+  const bf16_t* R1 = (const bf16_t*)a.r;
+  const bf16_t* R2 = (const bf16_t*)a.r2;
+  const int s_rl = tid >> 3, s_cc = tid & 7;   // store phase: row lane (0..63), 8-col chunk
+#pragma unroll
+  for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
+    const int cbase = pass * EPI_COLS;
+    if (wn * WN + WN > cbase && wn * WN < cbase + EPI_COLS) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * WN + j * 16 + lr;
+        if (col >= cbase && col < cbase + EPI_COLS) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              stage[(wm * WM + i * 16 + lq * 4 + r) * EPI_LD + (col - cbase)] = acc[i][j][r];
+        }
+      }
+    }
+    __syncthreads();
+    const int n = n0 + cbase + s_cc * 8;
+    if (n < a.Co) {   // Co % 8 == 0 on this path
+#pragma unroll
+      for (int rr = 0; rr < BM / 64; ++rr) {
+        const int row = s_rl + 64 * rr;
+        const long m = m0 + row;
+        if (m < M) {
+          const float* sp = stage + row * EPI_LD + s_cc * 8;
+          const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
+          float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          if (R1) {
+            float u[8];
+            Vec8<bf16_t>::load(R1 + (size_t)m * a.ldr + n, u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += u[e];
+          }
+          if (R2) {
+            float u[8];
+            Vec8<bf16_t>::load(R2 + (size_t)m * a.ldr2 + n, u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += u[e];
+          }
+          Vec8<bf16_t>::store(Y + (size_t)m * a.ldy + n, v);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int BN, int WMW, int WNW, int STAGES, int ST>
+hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
+  constexpr int BM = 256;
+  constexpr int STAGE_BYTES = (BM + BN) * 128;
+  constexpr int EPI = BM * (64 + 4) * 4 + 64 * 8 * 8 * 4;
+  constexpr int LDS = STAGES * STAGE_BYTES > EPI ? STAGES * STAGE_BYTES : EPI;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  long M = (long)a.N * a.Ho * a.Wo;
+  int nwg = ceil_div(M, BM) * ceil_div(a.Co, BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(V2_THREADS), LDS, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// bf16 fast path: C % 64 == 0, ld/co multiples of 8; stats tiles are 256 rows
+bool conv_nt_v2_ok(const ConvArgs& a) {
+  return (a.st == 1 || a.st == 2) && (a.C % BK) == 0 && (a.ldx % 8) == 0 && (a.ldw % 8) == 0 && (a.Co % 8) == 0 &&
+         (a.ldy % 8) == 0 && (!a.r || a.ldr % 8 == 0) && (!a.r2 || a.ldr2 % 8 == 0);
+}
+
+template <int ST>
+hipError_t v2_dispatch(const ConvArgs& a, hipStream_t s) {
+  if (a.Co > 128) return v2_launch<256, 4, 2, 2, ST>(a, s);
+  if (a.Co > 64) return v2_launch<128, 4, 2, 3, ST>(a, s);
+  return v2_launch<64, 8, 1, 3, ST>(a, s);
+}
+
+hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s) {
+  if (a.st == 1) return v2_dispatch<1>(a, s);
+  if (a.st == 2) return v2_dispatch<2>(a, s);
+  return hipErrorInvalidValue;
+}
+
+// ======================================================================================
+// bf16 weight gradient ("TN"), v2: C[co][tap*Ci+ci] = sum_p dy[p][co] * x[src(p,tap)][ci]
+//  * 512 threads = 8 waves (2 x 4), block tile BM co x BN (tap,ci) columns, K-step 64
+//    pixels, 3-stage LDS ring filled by LDS-DMA (counted vmcnt across raw barriers);
+//  * both operands are pixel-major: LDS rows are pixels; a lane's column chunk (and so its
+//    (tap, ci) decode) is fixed for the whole launch, only the pixel advances; padding taps
+//    and pixels past the split read the zero buffer;
+//  * rows are XOR-swizzled on 16-B chunks (chunk ^ (2*(r&3) + 8*((r>>3)&1))) so the
+//    ds_read_b64_tr_b16 transposed fragment reads (8 pixels of one column per lane) are
+//    bank-conflict free;
+//  * split-K over pixels into fp32 slabs (reduced in fixed order by splitk_reduce).
+// ======================================================================================
+namespace {
+
+constexpr int WG_THREADS = 512;
+constexpr int WBK = 64;  // pixels per K-step
+
+template <int COLS>
+__device__ __forceinline__ int wswz(int row, int ch) {
+  if constexpr (COLS >= 128) return ch ^ (2 * (row & 3) + 8 * ((row >> 3) & 1));
+  else return ch ^ (2 * (row & 3));
+}
+
+template <int BM, int BN, int WMW, int WNW>
+__global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs a) {
+  constexpr int ROWB_A = BM * 2, ROWB_B = BN * 2;            // bytes per pixel row
+  constexpr int CPR_A = BM / 8, CPR_B = BN / 8;              // 16-B chunks per row
+  constexpr int RPI_A = 64 / CPR_A, RPI_B = 64 / CPR_B;      // rows per wave-instruction
+  constexpr int AI = WBK * CPR_A / WG_THREADS;               // glds per lane per K-step
+  constexpr int BI = WBK * CPR_B / WG_THREADS;
+  constexpr int LPK = AI + BI;
+  constexpr int A_BYTES = WBK * ROWB_A, B_BYTES = WBK * ROWB_B;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int STAGES = 3;
+  constexpr int WM = BM / WMW, WN = BN / WNW;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  static_assert(WMW * WNW == 8, "8 waves");
+  static_assert(AI >= 1 && BI >= 1, "tile too small");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int m0 = blockIdx.x * BM;   // co
+  const int n0 = blockIdx.y * BN;   // (tap, ci)
+  const int Ncol = a.KH * a.KW * a.C;
+  const int P = a.N * a.Ho * a.Wo;
+  const int chunk = ((P + a.splits - 1) / a.splits + WBK - 1) / WBK * WBK;
+  const int p_begin = blockIdx.z * chunk;
+  const int p_end = (p_begin + chunk < P) ? p_begin + chunk : P;
+  const int nk = p_end > p_begin ? (p_end - p_begin + WBK - 1) / WBK : 0;
+  const bf16_t* DY = (const bf16_t*)a.dy;
+  const bf16_t* X = (const bf16_t*)a.x;
+  const bf16_t* zero = g_zero16;
+
+  // ---- launch-invariant per-lane decode ----
+  int a_row[AI], a_co[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    a_row[i] = (i * 8 + wave) * RPI_A + lane / CPR_A;
+    a_co[i] = m0 + wswz<BM>(a_row[i], lane % CPR_A) * 8;
+  }
+  int b_row[BI], b_dh[BI], b_dw[BI], b_ci[BI];
+  bool b_ok[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    b_row[i] = (i * 8 + wave) * RPI_B + lane / CPR_B;
+    const int col = n0 + wswz<BN>(b_row[i], lane % CPR_B) * 8;
+    b_ok[i] = col < Ncol;
+    const int cc = b_ok[i] ? col : 0;
+    const int tap = cc / a.C;
+    b_ci[i] = cc - tap * a.C;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    b_dh[i] = kh * a.dil - a.pad_h;
+    b_dw[i] = kw * a.dil - a.pad_w;
+  }
+
+  auto issue = [&](int kb, int stg) {
+    const int p0 = p_begin + kb * WBK;
+    char* sA = smem + stg * STAGE;
+    char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int p = p0 + a_row[i];
+      const bool ok = (p < p_end) & (a_co[i] < a.Co);
+      glds16(ok ? (const void*)(DY + (size_t)p * a.lddy + a_co[i]) : (const void*)zero,
+             sA + (i * 8 + wave) * 1024);
+    }
+    // pixel decode of the K-step's first pixel (wave-uniform), then per-row carries
+    const int wo0 = p0 % a.Wo, t0 = p0 / a.Wo;
+    const int ho0 = t0 % a.Ho, nn0 = t0 / a.Ho;
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int r = b_row[i];
+      const int p = p0 + r;
+      int wo = wo0 + r, ho = ho0, nn = nn0;
+      if (a.Wo >= WBK) {                 // at most one row carry
+        if (wo >= a.Wo) { wo -= a.Wo; if (++ho == a.Ho) { ho = 0; ++nn; } }
+      } else {
+        const int q = p;
+        wo = q % a.Wo;
+        const int t = q / a.Wo;
+        ho = t % a.Ho;
+        nn = t / a.Ho;
+      }
+      const int hi = ho * a.sf + b_dh[i], wi = wo * a.sf + b_dw[i];
+      const bool ok = (p < p_end) & b_ok[i] & ((unsigned)hi < (unsigned)a.H) &
+                      ((unsigned)wi < (unsigned)a.W);
+      const size_t off = ((size_t)((long)nn * a.H + hi) * a.W + wi) * a.ldx + b_ci[i];
+      glds16(ok ? (const void*)(X + off) : (const void*)zero, sB + (i * 8 + wave) * 1024);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int lq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  auto tr_read = [&](const char* base, int rowb, int row, int col) -> s16x4_t {
+    const int lc = col >> 3, within = (col & 7) * 2;
+    const int ph = rowb >= 256 ? lc ^ (2 * (row & 3) + 8 * ((row >> 3) & 1)) : lc ^ (2 * (row & 3));
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (s16x4_t __attribute__((address_space(3)))*)(base + row * rowb + ph * 16 + within));
+  };
+
+  auto compute = [&](int stg) {
+    const char* A = smem + stg * STAGE;
+    const char* B = A + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {     // two 32-pixel MFMA k-steps per stage
+      const int kr = 32 * s + 8 * lq + q4;
+      bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int col = wm * WM + i * 16 + 4 * p4;
+        s16x4_t lo = tr_read(A, ROWB_A, kr, col), hi = tr_read(A, ROWB_A, kr + 4, col);
+        short t8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        __builtin_memcpy(&af[i], t8, 16);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * WN + j * 16 + 4 * p4;
+        s16x4_t lo = tr_read(B, ROWB_B, kr, col), hi = tr_read(B, ROWB_B, kr + 4, col);
+        short t8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        __builtin_memcpy(&bfr[j], t8, 16);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int kb = 0; kb < nk; ++kb) {
+    if (kb + 1 < nk) wait_vmcnt<LPK>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kb + STAGES - 1 < nk) issue(kb + STAGES - 1, (kb + STAGES - 1) % STAGES);
+    compute(kb % STAGES);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  float* O = a.out + (size_t)blockIdx.z * a.Co * Ncol;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + i * 16 + lq * 4 + r;
+        if (m < a.Co && n < Ncol) O[(size_t)m * Ncol + n] = acc[i][j][r];
+      }
+    }
+}
+
+template <int BM, int BN, int WMW, int WNW>
+hipError_t wg2_launch(const WgradArgs& a, hipStream_t s) {
+  constexpr int LDS = 3 * WBK * (BM + BN) * 2;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  auto kern = conv_wgrad_v2_kernel<BM, BN, WMW, WNW>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int Ncol = a.KH * a.KW * a.C;
+  dim3 grid(ceil_div(a.Co, BM), ceil_div(Ncol, BN), a.splits);
+  hipLaunchKernelGGL(kern, grid, dim3(WG_THREADS), LDS, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool conv_wgrad_v2_ok(const WgradArgs& a) {
+  return (a.C % 8) == 0 && (a.ldx % 8) == 0 && (a.Co % 8) == 0 && (a.lddy % 8) == 0 &&
+         (long)a.N * a.Ho * a.Wo < (1L << 31);
+}
+
+// tile (BM co x BN cols) chosen so that the per-split work covers the co / column extents
+void conv_wgrad_v2_tile(int Co, int Ncol, int* bm, int* bn) {
+  *bm = Co <= 64 ? 64 : 128;
+  *bn = Ncol <= 64 ? 64 : (Ncol <= 128 ? 128 : 256);
+}
+
+hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s) {
+  int bm, bn;
+  conv_wgrad_v2_tile(a.Co, a.KH * a.KW * a.C, &bm, &bn);
+  if (bm == 64) {
+    if (bn == 64) return wg2_launch<64, 64, 4, 2>(a, s);
+    if (bn == 128) return wg2_launch<64, 128, 2, 4>(a, s);
+    return wg2_launch<64, 256, 2, 4>(a, s);
+  }
+  if (bn == 64) return wg2_launch<128, 64, 4, 2>(a, s);
+  if (bn == 128) return wg2_launch<128, 128, 4, 2>(a, s);
+  return wg2_launch<128, 256, 2, 4>(a, s);
+}

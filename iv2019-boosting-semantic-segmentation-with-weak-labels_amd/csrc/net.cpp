@@ -326,11 +326,13 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
 }
 
 int wgrad_splits(const ConvL& L) {
-  const int BM = L.co_pad <= 64 ? 64 : 128;
-  const int BN = 128;
+  int BM = L.co_pad <= 64 ? 64 : 128;
+  int BN = 128;
+  if (L.ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, L.k * L.k * L.ci, &BM, &BN);
   long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * L.ci + BN - 1) / BN);
   long P = (long)L.N * L.Ho * L.Wo;
-  long s = std::max<long>(1, 1024 / std::max<long>(tiles, 1));
+  // ~2 waves of 256 single-workgroup CUs, each split >= 32 K-steps of 64 pixels
+  long s = std::max<long>(1, 512 / std::max<long>(tiles, 1));
   long maxs = std::max<long>(1, P / 2048);
   s = std::min(s, maxs);
   return (int)std::min<long>(s, 256);
@@ -376,7 +378,7 @@ int conv_forward(Step& S, int li, const Act& x) {
   if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
   HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
-  HIPCALL(c, launch_bn_stats_finalize(L.stats_part, M, L.co, 128, c->stat_scratch,
+  HIPCALL(c, launch_bn_stats_finalize(L.stats_part, M, L.co, conv_nt_stat_rows(S.dt, 0, a), c->stat_scratch,
                                       c->params + L.g_off, L.st, S.s));
   return 0;
 }
@@ -1106,6 +1108,23 @@ int seg_profile_read(seg_ctx* c, int cls, double* ms_total, double* gflop_total,
   return 0;
 }
 
+int seg_profile_dump(seg_ctx* c, char* buf, int len) {
+  if (!c || !buf || len <= 0) return set_err(c ? &c->err : nullptr, -EINVAL, "bad argument");
+  std::string out;
+  char line[512];
+  for (auto& r : c->prof.recs) {
+    HIPCALL(c, hipEventSynchronize(c->prof.ev[r.e1]));
+    float ms = 0;
+    HIPCALL(c, hipEventElapsedTime(&ms, c->prof.ev[r.e0], c->prof.ev[r.e1]));
+    const ConvL& L = c->convs[r.layer];
+    snprintf(line, sizeof(line), "%d %s %d %d %d %d %d %d %.6f %.6f\n", r.cls, L.name.c_str(), L.ci,
+             L.co, L.k, L.rate, L.Ho, L.Wo, r.gflop, (double)ms);
+    out += line;
+  }
+  snprintf(buf, len, "%s", out.c_str());
+  return (int)out.size() >= len ? -ENOSPC : 0;
+}
+
 static void op_geom(int H, int W, int k, int stride, int rate, int explicit_pad, int* Ho, int* Wo,
                     int* ph, int* pw) {
   ConvL L;
@@ -1125,6 +1144,12 @@ int seg_op_conv_fwd(int dtype, const void* x, int N, int H, int W, int C, int ld
   a.KH = a.KW = k; a.sf = stride; a.st = 1; a.pad_h = ph; a.pad_w = pw; a.dil = rate; a.stats = stats;
   hipError_t e = launch_conv_nt(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, 0, a, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_fwd");
+}
+
+int seg_op_conv_stat_rows(int dtype, int C, int ldx, int Co, int ldy) {
+  ConvArgs a{};
+  a.C = C; a.ldx = ldx; a.Co = Co; a.ldy = ldy; a.ldw = 8; a.st = 1;
+  return conv_nt_stat_rows(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, 0, a);
 }
 
 int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,

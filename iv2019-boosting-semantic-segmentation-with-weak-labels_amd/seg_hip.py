@@ -21,8 +21,9 @@ EXPORTED_SYMBOLS = [
     "seg_create", "seg_destroy", "seg_last_error", "seg_sizes", "seg_bind_buffers",
     "seg_param_count", "seg_param_info", "seg_param_shape", "seg_params_updated", "seg_forward", "seg_loss",
     "seg_backward", "seg_apply_update", "seg_outputs", "seg_confusion", "seg_debug_tensor",
-    "seg_profile",
-    "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_dgrad", "seg_op_conv_wgrad",
+    "seg_profile", "seg_profile_dump",
+    "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
+    "seg_op_conv_wgrad",
 ]
 
 PYRAMID = {"none": 0, "psp": 1, "aspp": 2}
@@ -73,10 +74,12 @@ def _load():
         "seg_debug_tensor": (ip, [vp, ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(ip),
                                   ctypes.POINTER(ip), ctypes.POINTER(ip)]),
         "seg_profile": (ip, [vp, ip]),
+        "seg_profile_dump": (ip, [vp, ctypes.c_char_p, ip]),
         "seg_profile_read": (ip, [vp, ip, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                   ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ip]),
         "seg_op_conv_fwd": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, vp, ip, vp, vp]),
+        "seg_op_conv_stat_rows": (ip, [ip, ip, ip, ip, ip]),
         "seg_op_conv_dgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, vp,
                                    ip, vp]),
         "seg_op_conv_wgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, ip,
@@ -251,6 +254,18 @@ class SegContext:
                                    ctypes.byref(mx), name, 256), self.h)
         return dict(ms=ms.value, gflop=gf.value, launches=n.value, ms_max_layer=mx.value,
                     max_layer=name.value.decode())
+
+    def profile_dump(self):
+        """Per-launch records of the conv kernels: list of dicts."""
+        buf = ctypes.create_string_buffer(1 << 22)
+        check(LIB.seg_profile_dump(self.h, buf, len(buf)), self.h)
+        rows = []
+        for line in buf.value.decode().splitlines():
+            f = line.split()
+            rows.append(dict(cls=int(f[0]), name=f[1], ci=int(f[2]), co=int(f[3]), k=int(f[4]),
+                             rate=int(f[5]), ho=int(f[6]), wo=int(f[7]), gflop=float(f[8]),
+                             ms=float(f[9])))
+        return rows
 
     def close(self):
         if getattr(self, "h", None):

@@ -78,8 +78,10 @@ def test_conv_fwd(cuda, dtype, case):
     tol = 1e-4 if dtype == "fp32" else 2e-2
     assert _rel(y, ref) < tol
     # BN partial statistics: merge (sum, M2 about the tile mean) and compare
-    st = stats.cpu().numpy().astype(np.float64)
-    cnt = np.minimum(128, M - np.arange(st.shape[0]) * 128).astype(np.float64)
+    tr = LIB.seg_op_conv_stat_rows(1 if dtype == "bf16" else 0, Ci, Ci, Co, Co)
+    nt = (M + tr - 1) // tr
+    st = stats.cpu().numpy().astype(np.float64)[:nt]
+    cnt = np.minimum(tr, M - np.arange(nt) * tr).astype(np.float64)
     mean = st[:, :, 0].sum(0) / M
     tile_mean = st[:, :, 0] / cnt[:, None]
     m2 = st[:, :, 1].sum(0) + (cnt[:, None] * (tile_mean - mean) ** 2).sum(0)
