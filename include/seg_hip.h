@@ -106,7 +106,8 @@ int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions,
  * dims = N, H, W, C; ld = pixel stride; dtype = SEG_DTYPE_* of the storage */
 int seg_debug_tensor(seg_ctx* ctx, const char* name, void** ptr, int* dims, int* ld, int* dtype);
 
-/* kernel-time profiling of conv classes (0 fwd, 1 dgrad, 2 wgrad) ---------------------- */
+/* kernel-time profiling: conv classes 0 fwd, 1 dgrad, 2 wgrad (gflop = algorithmic flops);
+ * BN classes 3 apply, 4 bwd reduce, 5 bwd apply (gflop field = algorithmic GB moved) ---- */
 int seg_profile(seg_ctx* ctx, int enable);
 int seg_profile_read(seg_ctx* ctx, int cls, double* ms_total, double* gflop_total,
                      int64_t* launches, double* ms_max_layer, char* layer_name, int name_len);

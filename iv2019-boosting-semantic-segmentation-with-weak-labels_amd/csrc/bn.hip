@@ -270,6 +270,211 @@ __global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
   }
 }
 
+// ---- 8-channel streaming kernels (C % 8 == 0): thread -> fixed channel group ------------
+// A thread owns one 8-channel group for the whole launch (per-channel constants loaded once)
+// and walks rows; U rows are loaded before any is consumed, so U x (2..3) 16-B loads are in
+// flight per lane. No integer division in the row loop. C/8 > 256 spills into blockIdx.y.
+constexpr int BN_U = 4;
+
+struct RowLane {
+  int cg, rl, rpp;
+  bool act;
+};
+
+__device__ __forceinline__ RowLane row_lane(int cg_n) {
+  RowLane r;
+  if (cg_n >= 256) {
+    r.cg = blockIdx.y * 256 + threadIdx.x; r.rl = 0; r.rpp = 1; r.act = r.cg < cg_n;
+  } else {
+    r.rpp = 256 / cg_n; r.cg = threadIdx.x % cg_n; r.rl = threadIdx.x / cg_n; r.act = r.rl < r.rpp;
+  }
+  return r;
+}
+
+// per-channel constants: scalar loads (BN vectors of small heads break 16-B alignment)
+__device__ __forceinline__ void ld8(const float* p, int c0, float* o) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = p[c0 + e];
+}
+
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void bn_apply8_kernel(BnApplyArgs a) {
+  const RowLane L = row_lane(a.C / 8);
+  if (!L.act) return;
+  const int c0 = L.cg * 8;
+  float mu[8], sc[8], be[8], mu2[8], sc2[8], be2[8];
+  ld8(a.mean, c0, mu); ld8(a.scale, c0, sc); ld8(a.beta, c0, be);
+  const T* Y = (const T*)a.y;
+  const T* RES = (const T*)a.res;
+  const T* Y2 = (const T*)a.y2;
+  TO* O = (TO*)a.out;
+  if (Y2) { ld8(a.mean2, c0, mu2); ld8(a.scale2, c0, sc2); ld8(a.beta2, c0, be2); }
+  const long step = (long)L.rpp * BN_U;
+  for (long base = (long)blockIdx.x * step; base < a.M; base += (long)gridDim.x * step) {
+    float v[BN_U][8], u[BN_U][8];
+#pragma unroll
+    for (int k = 0; k < BN_U; ++k) {
+      const long m = base + k * L.rpp + L.rl;
+      if (m < a.M) Vec8<T>::load(Y + (size_t)m * a.ldy + c0, v[k]);
+    }
+    if (Y2 || RES) {
+#pragma unroll
+      for (int k = 0; k < BN_U; ++k) {
+        const long m = base + k * L.rpp + L.rl;
+        if (m >= a.M) continue;
+        if (Y2) {
+          Vec8<T>::load(Y2 + (size_t)m * a.ldy2 + c0, u[k]);
+        } else {
+          size_t rm = (size_t)m;
+          if (a.rs > 1) {
+            const int mi = (int)m;
+            const int wo = mi % a.Wo, t = mi / a.Wo;
+            const int ho = t % a.Ho, n = t / a.Ho;
+            rm = ((size_t)n * a.Hr + (size_t)ho * a.rs) * a.Wr + (size_t)wo * a.rs;
+          }
+          Vec8<T>::load(RES + rm * a.ldres + c0, u[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < BN_U; ++k) {
+      const long m = base + k * L.rpp + L.rl;
+      if (m >= a.M) continue;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = (v[k][e] - mu[e]) * sc[e] + be[e];
+        if (Y2) x = ((u[k][e] - mu2[e]) * sc2[e] + be2[e]) + x;
+        else if (RES) x = u[k][e] + x;
+        o[e] = a.relu ? fmaxf(x, 0.f) : x;
+      }
+      Vec8<TO>::store(O + (size_t)m * a.ldo + c0, o);
+    }
+  }
+}
+
+// masked incoming gradient for U rows (dz * [z > 0] * dzscale)
+template <typename T, typename TZ>
+__device__ __forceinline__ void bwd_load(const BnBwdArgs& a, const RowLane& L, int c0, long base,
+                                         float (&dz)[BN_U][8], float (&y)[BN_U][8]) {
+  const TZ* DZ = (const TZ*)a.dz;
+  const TZ* Z = (const TZ*)a.z;
+  const T* Y = (const T*)a.y;
+  float z[BN_U][8];
+#pragma unroll
+  for (int k = 0; k < BN_U; ++k) {
+    const long m = base + k * L.rpp + L.rl;
+    if (m < a.M) {
+      Vec8<TZ>::load(DZ + (size_t)m * a.lddz + c0, dz[k]);
+      Vec8<T>::load(Y + (size_t)m * a.ldy + c0, y[k]);
+      if (Z) Vec8<TZ>::load(Z + (size_t)m * a.ldz + c0, z[k]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { dz[k][e] = 0.f; y[k][e] = 0.f; z[k][e] = 0.f; }
+    }
+  }
+  if (Z) {
+#pragma unroll
+    for (int k = 0; k < BN_U; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dz[k][e] = z[k][e] > 0.f ? dz[k][e] : 0.f;
+  }
+  if (a.dzscale) {
+    float ds[8];
+    ld8(a.dzscale, c0, ds);
+#pragma unroll
+    for (int k = 0; k < BN_U; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dz[k][e] *= ds[e];
+  }
+}
+
+// per row block partial (sum dyhat, sum dyhat*xhat); rows of block b: [b*rows_per, ...)
+template <typename T, typename TZ>
+__global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
+  __shared__ float sh[2][256 * 8];
+  const RowLane L = row_lane(a.C / 8);
+  const int c0 = (L.act ? L.cg : 0) * 8;
+  const long rows_per = (a.M + a.rb - 1) / a.rb;
+  const long r0 = (long)blockIdx.x * rows_per;
+  const long r1 = (r0 + rows_per < a.M) ? r0 + rows_per : a.M;
+  float s1[8], s2[8], mu[8], inv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  if (L.act) {
+    ld8(a.mean, c0, mu); ld8(a.invstd, c0, inv);
+    BnBwdArgs b = a;
+    b.M = r1;   // rows past the block's range read as zero
+    for (long base = r0; base < r1; base += (long)L.rpp * BN_U) {
+      float dz[BN_U][8], y[BN_U][8];
+      bwd_load<T, TZ>(b, L, c0, base, dz, y);
+#pragma unroll
+      for (int k = 0; k < BN_U; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += dz[k][e];
+          s2[e] += dz[k][e] * ((y[k][e] - mu[e]) * inv[e]);
+        }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sh[0][threadIdx.x * 8 + e] = s1[e];
+    sh[1][threadIdx.x * 8 + e] = s2[e];
+  }
+  __syncthreads();
+  if (L.act && L.rl == 0) {
+    const int cg_b = a.C / 8 >= 256 ? 256 : a.C / 8;
+    for (int r = 1; r < L.rpp; ++r) {
+      const int t = r * cg_b + threadIdx.x;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] += sh[0][t * 8 + e]; s2[e] += sh[1][t * 8 + e]; }
+    }
+    float* o = a.part + 2 * ((size_t)blockIdx.x * a.C + c0);
+#pragma unroll
+    for (int e = 0; e < 8; e += 2)
+      *(float4*)(o + 2 * e) = make_float4(s1[e], s2[e], s1[e + 1], s2[e + 1]);
+  }
+}
+
+template <typename T, typename TZ>
+__global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwdArgs a) {
+  const RowLane L = row_lane(a.C / 8);
+  if (!L.act) return;
+  const int c0 = L.cg * 8;
+  float mu[8], inv[8], sc[8], sdy[8], sdyx[8];
+  ld8(a.mean, c0, mu); ld8(a.invstd, c0, inv); ld8(a.scale, c0, sc);
+  ld8(a.sdy, c0, sdy); ld8(a.sdyx, c0, sdyx);
+  T* DY = (T*)a.dy;
+  T* DH = (T*)a.dyhat;
+  const long step = (long)L.rpp * BN_U;
+  for (long base = (long)blockIdx.x * step; base < a.M; base += (long)gridDim.x * step) {
+    float dz[BN_U][8], y[BN_U][8];
+    bwd_load<T, TZ>(a, L, c0, base, dz, y);
+#pragma unroll
+    for (int k = 0; k < BN_U; ++k) {
+      const long m = base + k * L.rpp + L.rl;
+      if (m >= a.M) continue;
+      if (DH) Vec8<T>::store(DH + (size_t)m * a.lddyhat + c0, dz[k]);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (y[k][e] - mu[e]) * inv[e];
+        o[e] = sc[e] * (dz[k][e] - sdy[e] - xh * sdyx[e]);
+      }
+      Vec8<T>::store(DY + (size_t)m * a.lddy + c0, o);
+    }
+  }
+}
+
+dim3 grid8(long M, int C) {
+  const int cg_n = C / 8;
+  const int rpp = cg_n >= 256 ? 1 : 256 / cg_n;
+  long g = (M + (long)rpp * BN_U - 1) / ((long)rpp * BN_U);
+  if (g > 2048) g = 2048;
+  return dim3((unsigned)(g < 1 ? 1 : g), cg_n > 256 ? (unsigned)ceil_div(cg_n, 256) : 1u);
+}
+
 __global__ void moving_update_kernel(float* mm, float* mv, const float* bm, const float* bv, int n,
                                      float decay) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -289,7 +494,7 @@ hipError_t apply_t(const BnApplyArgs& a, hipStream_t s) {
   bool v8 = (a.C % 8 == 0) && (a.ldy % 8 == 0) && (a.ldo % 8 == 0) &&
             (!a.res || a.ldres % 8 == 0) && (!a.y2 || a.ldy2 % 8 == 0) &&
             (((uintptr_t)a.out) % 16 == 0);
-  if (v8) hipLaunchKernelGGL((bn_apply_kernel<T, TO, 8>), dim3(grid_for(a.M * a.C / 8)), dim3(256), 0, s, a);
+  if (v8) hipLaunchKernelGGL((bn_apply8_kernel<T, TO>), grid8(a.M, a.C), dim3(256), 0, s, a);
   else hipLaunchKernelGGL((bn_apply_kernel<T, TO, 1>), dim3(grid_for(a.M * a.C)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
@@ -303,14 +508,18 @@ bool bwd_v8(const BnBwdArgs& a) {
 
 template <typename T, typename TZ>
 hipError_t bwd_reduce_t(const BnBwdArgs& a, hipStream_t s) {
-  if (bwd_v8<T, TZ>(a)) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, TZ, 8>), dim3(a.rb), dim3(256), 0, s, a);
+  if (bwd_v8<T, TZ>(a)) {
+    const int cg_n = a.C / 8;
+    hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ>), dim3(a.rb, cg_n > 256 ? ceil_div(cg_n, 256) : 1),
+                       dim3(256), 0, s, a);
+  }
   else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, TZ, 1>), dim3(a.rb), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 template <typename T, typename TZ>
 hipError_t bwd_apply_t(const BnBwdArgs& a, hipStream_t s) {
-  if (bwd_v8<T, TZ>(a)) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, TZ, 8>), dim3(grid_for(a.M * a.C / 8)), dim3(256), 0, s, a);
+  if (bwd_v8<T, TZ>(a)) hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ>), grid8(a.M, a.C), dim3(256), 0, s, a);
   else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, TZ, 1>), dim3(grid_for(a.M * a.C)), dim3(256), 0, s, a);
   return hipGetLastError();
 }

@@ -402,8 +402,13 @@ int bn_apply(Step& S, int li, const Act& out, int out_f32, const Act* res = null
     a.beta2 = c->params + L2.b_off;
   }
   a.out = out.p; a.ldo = out.ld;
+  const double esz = S.dt == SEG_BF16 ? 2.0 : 4.0;
+  const double gb = a.M * (double)a.C * (esz * (1 + (a.res || a.y2 ? 1 : 0) + (a.y2 ? 1 : 0)) +
+                                         (out_f32 ? 4.0 : esz)) * 1e-9;
+  int slot;
+  if (int r = prof_begin(c, S.s, 3, li, gb, &slot)) return r;
   HIPCALL(c, launch_bn_apply(S.dt, out_f32, a, S.s));
-  return 0;
+  return prof_end(c, S.s, slot);
 }
 
 // BN backward for layer li: dz (gradient wrt BN output), z (mask source or null)
@@ -421,13 +426,20 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   if (dyhat_out) { a.dyhat = dyhat_out->p; a.lddyhat = dyhat_out->ld; }
   a.part = L.bwd_part; a.rb = L.rb;
   a.dzscale = dzscale;
+  const double esz = S.dt == SEG_BF16 ? 2.0 : 4.0, zsz = dz_f32 ? 4.0 : esz;
+  const double me = a.M * (double)a.C * 1e-9;
+  const double gb_in = me * (zsz * (z ? 2 : 1) + esz);
+  int slot;
+  if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
   HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
   const bool tb = c->cfg.train_bn != 0;
   HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
                                     tb ? c->grads + L.g_off : nullptr,
                                     tb ? c->grads + L.b_off : nullptr, S.s));
+  if (int r = prof_begin(c, S.s, 5, li, gb_in + me * esz * (dyhat_out ? 2 : 1), &slot)) return r;
   HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
-  return 0;
+  return prof_end(c, S.s, slot);
 }
 
 // dx = dgrad(dy) [+ r1] [+ r2]

@@ -69,10 +69,11 @@ CONFIGS = [
     SegConfig(height=64, width=128, nb_pp=2, pyramid="psp"),
     SegConfig(height=64, width=96, nb_pp=1, nb_pb=1, nb_pi=1, pyramid="psp"),
     SegConfig(height=48, width=64, nb_pp=1, pyramid="none"),
+    SegConfig(depth=101, height=48, width=64, nb_pp=1, nb_pb=1, pyramid="psp"),
 ]
 
 
-@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}")
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"r{c.depth}-{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}")
 def test_train_step_fp32(cuda, cfg):
     from input_pipelines.synthetic import batch
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=3).items()}
