@@ -1,5 +1,6 @@
 // Batch-norm kernels (see bn.h). All reductions use a fixed order: bitwise reproducible.
 #include "bn.h"
+#include <type_traits>
 
 namespace {
 
@@ -274,7 +275,7 @@ __global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
 // A thread owns one 8-channel group for the whole launch (per-channel constants loaded once)
 // and walks rows; U rows are loaded before any is consumed, so U x (2..3) 16-B loads are in
 // flight per lane. No integer division in the row loop. C/8 > 256 spills into blockIdx.y.
-constexpr int BN_U = 4;
+constexpr int BN_U = 4;   // rows in flight per thread (reduce combines 4 slots explicitly)
 
 struct RowLane {
   int cg, rl, rpp;
@@ -297,89 +298,120 @@ __device__ __forceinline__ void ld8(const float* p, int c0, float* o) {
   for (int e = 0; e < 8; ++e) o[e] = p[c0 + e];
 }
 
-template <typename T, typename TO>
+// Row loops are split into full groups (U valid rows: no bounds tests, all loads issued
+// before any use) and one guarded tail group, and every optional input is a template
+// parameter, so the compiler emits straight-line load batches.
+enum { RES_NONE = 0, RES_PLAIN = 1, RES_SUB = 2, RES_BN2 = 3 };
+
+template <typename T, typename TO, int RES, int RELU>
 __global__ __launch_bounds__(256) void bn_apply8_kernel(BnApplyArgs a) {
   const RowLane L = row_lane(a.C / 8);
   if (!L.act) return;
   const int c0 = L.cg * 8;
   float mu[8], sc[8], be[8], mu2[8], sc2[8], be2[8];
   ld8(a.mean, c0, mu); ld8(a.scale, c0, sc); ld8(a.beta, c0, be);
-  const T* Y = (const T*)a.y;
-  const T* RES = (const T*)a.res;
-  const T* Y2 = (const T*)a.y2;
-  TO* O = (TO*)a.out;
-  if (Y2) { ld8(a.mean2, c0, mu2); ld8(a.scale2, c0, sc2); ld8(a.beta2, c0, be2); }
+  if constexpr (RES == RES_BN2) { ld8(a.mean2, c0, mu2); ld8(a.scale2, c0, sc2); ld8(a.beta2, c0, be2); }
+  const T* Y = (const T*)a.y + c0;
+  const T* RS = (const T*)(RES == RES_BN2 ? a.y2 : a.res) + c0;
+  const int ldr = RES == RES_BN2 ? a.ldy2 : a.ldres;
+  TO* O = (TO*)a.out + c0;
   const long step = (long)L.rpp * BN_U;
-  for (long base = (long)blockIdx.x * step; base < a.M; base += (long)gridDim.x * step) {
+  auto res_row = [&](long m) -> size_t {
+    if constexpr (RES == RES_SUB) {
+      const int mi = (int)m;
+      const int wo = mi % a.Wo, t = mi / a.Wo;
+      const int ho = t % a.Ho, n = t / a.Ho;
+      return ((size_t)n * a.Hr + (size_t)ho * a.rs) * a.Wr + (size_t)wo * a.rs;
+    } else {
+      return (size_t)m;
+    }
+  };
+  auto body = [&](long base, int nrows) {
     float v[BN_U][8], u[BN_U][8];
 #pragma unroll
-    for (int k = 0; k < BN_U; ++k) {
-      const long m = base + k * L.rpp + L.rl;
-      if (m < a.M) Vec8<T>::load(Y + (size_t)m * a.ldy + c0, v[k]);
-    }
-    if (Y2 || RES) {
+    for (int k = 0; k < BN_U; ++k)
+      if (k < nrows) Vec8<T>::load(Y + (size_t)(base + k * L.rpp) * a.ldy, v[k]);
+    if constexpr (RES != RES_NONE) {
 #pragma unroll
-      for (int k = 0; k < BN_U; ++k) {
-        const long m = base + k * L.rpp + L.rl;
-        if (m >= a.M) continue;
-        if (Y2) {
-          Vec8<T>::load(Y2 + (size_t)m * a.ldy2 + c0, u[k]);
-        } else {
-          size_t rm = (size_t)m;
-          if (a.rs > 1) {
-            const int mi = (int)m;
-            const int wo = mi % a.Wo, t = mi / a.Wo;
-            const int ho = t % a.Ho, n = t / a.Ho;
-            rm = ((size_t)n * a.Hr + (size_t)ho * a.rs) * a.Wr + (size_t)wo * a.rs;
-          }
-          Vec8<T>::load(RES + rm * a.ldres + c0, u[k]);
-        }
-      }
+      for (int k = 0; k < BN_U; ++k)
+        if (k < nrows) Vec8<T>::load(RS + res_row(base + k * L.rpp) * ldr, u[k]);
     }
 #pragma unroll
     for (int k = 0; k < BN_U; ++k) {
-      const long m = base + k * L.rpp + L.rl;
-      if (m >= a.M) continue;
+      if (k >= nrows) continue;
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float x = (v[k][e] - mu[e]) * sc[e] + be[e];
-        if (Y2) x = ((u[k][e] - mu2[e]) * sc2[e] + be2[e]) + x;
-        else if (RES) x = u[k][e] + x;
-        o[e] = a.relu ? fmaxf(x, 0.f) : x;
+        float x = __builtin_fmaf(v[k][e] - mu[e], sc[e], be[e]);   // = conv_v2 fused mask
+        if constexpr (RES == RES_BN2) x = __builtin_fmaf(u[k][e] - mu2[e], sc2[e], be2[e]) + x;
+        else if constexpr (RES != RES_NONE) x = u[k][e] + x;
+        o[e] = RELU ? fmaxf(x, 0.f) : x;
       }
-      Vec8<TO>::store(O + (size_t)m * a.ldo + c0, o);
+      Vec8<TO>::store(O + (size_t)(base + k * L.rpp) * a.ldo, o);
     }
-  }
+  };
+  long base = (long)blockIdx.x * step + L.rl;
+  for (; base + (BN_U - 1) * L.rpp < a.M; base += (long)gridDim.x * step) body(base, BN_U);
+  if (base < a.M) body(base, (int)((a.M - base + L.rpp - 1) / L.rpp));
 }
 
-// masked incoming gradient for U rows (dz * [z > 0] * dzscale)
-template <typename T, typename TZ>
-__device__ __forceinline__ void bwd_load(const BnBwdArgs& a, const RowLane& L, int c0, long base,
+// raw 8-element row chunk: loaded first for every row of a group, converted afterwards, so
+// that all of a group's loads are in flight together
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16_t> {
+  uint4 u;
+  __device__ __forceinline__ void load(const bf16_t* p) { u = *(const uint4*)p; }
+  __device__ __forceinline__ void cvt(float* o) const {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[2 * i] = bf2f((bf16_t)(w[i] & 0xffff)); o[2 * i + 1] = bf2f((bf16_t)(w[i] >> 16)); }
+  }
+};
+template <> struct Raw8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p) { a = *(const float4*)p; b = *(const float4*)(p + 4); }
+  __device__ __forceinline__ void cvt(float* o) const {
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+};
+
+// masked incoming gradient for n rows (dz * [z > 0] * dzscale) and the matching y rows
+template <typename T, typename TZ, int HZ, int HS, bool FULL>
+__device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, int rpp, int nrows,
                                          float (&dz)[BN_U][8], float (&y)[BN_U][8]) {
-  const TZ* DZ = (const TZ*)a.dz;
-  const TZ* Z = (const TZ*)a.z;
-  const T* Y = (const T*)a.y;
-  float z[BN_U][8];
+  if constexpr (FULL) nrows = BN_U;
+  const TZ* DZ = (const TZ*)a.dz + c0;
+  const TZ* Z = (const TZ*)a.z + c0;
+  const T* Y = (const T*)a.y + c0;
+  Raw8<TZ> rdz[BN_U], rz[BN_U];
+  Raw8<T> ry[BN_U];
 #pragma unroll
   for (int k = 0; k < BN_U; ++k) {
-    const long m = base + k * L.rpp + L.rl;
-    if (m < a.M) {
-      Vec8<TZ>::load(DZ + (size_t)m * a.lddz + c0, dz[k]);
-      Vec8<T>::load(Y + (size_t)m * a.ldy + c0, y[k]);
-      if (Z) Vec8<TZ>::load(Z + (size_t)m * a.ldz + c0, z[k]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { dz[k][e] = 0.f; y[k][e] = 0.f; z[k][e] = 0.f; }
+    if (FULL || k < nrows) {
+      const size_t m = (size_t)(base + k * rpp);
+      rdz[k].load(DZ + m * a.lddz);
+      ry[k].load(Y + m * a.ldy);
+      if constexpr (HZ) rz[k].load(Z + m * a.ldz);
     }
   }
-  if (Z) {
+  __builtin_amdgcn_sched_barrier(0);   // keep the group's loads ahead of every conversion
 #pragma unroll
-    for (int k = 0; k < BN_U; ++k)
+  for (int k = 0; k < BN_U; ++k) {
+    if (FULL || k < nrows) {
+      rdz[k].cvt(dz[k]);
+      ry[k].cvt(y[k]);
+      if constexpr (HZ) {
+        float z[8];
+        rz[k].cvt(z);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) dz[k][e] = z[k][e] > 0.f ? dz[k][e] : 0.f;
+        for (int e = 0; e < 8; ++e) dz[k][e] = z[e] > 0.f ? dz[k][e] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { dz[k][e] = 0.f; y[k][e] = 0.f; }
+    }
   }
-  if (a.dzscale) {
+  if constexpr (HS) {
     float ds[8];
     ld8(a.dzscale, c0, ds);
 #pragma unroll
@@ -390,7 +422,7 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, const RowLane& L, i
 }
 
 // per row block partial (sum dyhat, sum dyhat*xhat); rows of block b: [b*rows_per, ...)
-template <typename T, typename TZ>
+template <typename T, typename TZ, int HZ, int HS>
 __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
   __shared__ float sh[2][256 * 8];
   const RowLane L = row_lane(a.C / 8);
@@ -399,23 +431,34 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
   const long r0 = (long)blockIdx.x * rows_per;
   const long r1 = (r0 + rows_per < a.M) ? r0 + rows_per : a.M;
   float s1[8], s2[8], mu[8], inv[8];
+  // one accumulator set per row slot k: the U rows of a group stay independent (no loop
+  // rerolling), so their loads are issued together
+  float t1[BN_U][8], t2[BN_U][8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (int k = 0; k < BN_U; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { t1[k][e] = 0.f; t2[k][e] = 0.f; }
   if (L.act) {
     ld8(a.mean, c0, mu); ld8(a.invstd, c0, inv);
-    BnBwdArgs b = a;
-    b.M = r1;   // rows past the block's range read as zero
-    for (long base = r0; base < r1; base += (long)L.rpp * BN_U) {
+    auto acc = [&](long base, int nrows, auto full) {
       float dz[BN_U][8], y[BN_U][8];
-      bwd_load<T, TZ>(b, L, c0, base, dz, y);
+      bwd_load<T, TZ, HZ, HS, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
 #pragma unroll
       for (int k = 0; k < BN_U; ++k)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          s1[e] += dz[k][e];
-          s2[e] += dz[k][e] * ((y[k][e] - mu[e]) * inv[e]);
+          t1[k][e] += dz[k][e];
+          t2[k][e] += dz[k][e] * ((y[k][e] - mu[e]) * inv[e]);
         }
-    }
+    };
+    long base = r0 + L.rl;
+    for (; base + (BN_U - 1) * L.rpp < r1; base += (long)L.rpp * BN_U) acc(base, BN_U, std::true_type{});
+    if (base < r1) acc(base, (int)((r1 - base + L.rpp - 1) / L.rpp), std::false_type{});
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s1[e] = (t1[0][e] + t1[1][e]) + (t1[2][e] + t1[3][e]);
+    s2[e] = (t2[0][e] + t2[1][e]) + (t2[2][e] + t2[3][e]);
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -437,7 +480,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
   }
 }
 
-template <typename T, typename TZ>
+template <typename T, typename TZ, int HZ, int HS, int HD>
 __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwdArgs a) {
   const RowLane L = row_lane(a.C / 8);
   if (!L.act) return;
@@ -445,26 +488,30 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwdArgs a) {
   float mu[8], inv[8], sc[8], sdy[8], sdyx[8];
   ld8(a.mean, c0, mu); ld8(a.invstd, c0, inv); ld8(a.scale, c0, sc);
   ld8(a.sdy, c0, sdy); ld8(a.sdyx, c0, sdyx);
-  T* DY = (T*)a.dy;
-  T* DH = (T*)a.dyhat;
+  T* DY = (T*)a.dy + c0;
+  T* DH = (T*)a.dyhat + c0;
   const long step = (long)L.rpp * BN_U;
-  for (long base = (long)blockIdx.x * step; base < a.M; base += (long)gridDim.x * step) {
+  auto body = [&](long base, int nrows, auto full) {
     float dz[BN_U][8], y[BN_U][8];
-    bwd_load<T, TZ>(a, L, c0, base, dz, y);
+    if constexpr (decltype(full)::value) nrows = BN_U;
+    bwd_load<T, TZ, HZ, HS, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
 #pragma unroll
     for (int k = 0; k < BN_U; ++k) {
-      const long m = base + k * L.rpp + L.rl;
-      if (m >= a.M) continue;
-      if (DH) Vec8<T>::store(DH + (size_t)m * a.lddyhat + c0, dz[k]);
+      if (k >= nrows) continue;
+      const size_t m = (size_t)(base + k * L.rpp);
+      if constexpr (HD) Vec8<T>::store(DH + m * a.lddyhat, dz[k]);
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xh = (y[k][e] - mu[e]) * inv[e];
         o[e] = sc[e] * (dz[k][e] - sdy[e] - xh * sdyx[e]);
       }
-      Vec8<T>::store(DY + (size_t)m * a.lddy + c0, o);
+      Vec8<T>::store(DY + m * a.lddy, o);
     }
-  }
+  };
+  long base = (long)blockIdx.x * step + L.rl;
+  for (; base + (BN_U - 1) * L.rpp < a.M; base += (long)gridDim.x * step) body(base, BN_U, std::true_type{});
+  if (base < a.M) body(base, (int)((a.M - base + L.rpp - 1) / L.rpp), std::false_type{});
 }
 
 dim3 grid8(long M, int C) {
@@ -494,7 +541,17 @@ hipError_t apply_t(const BnApplyArgs& a, hipStream_t s) {
   bool v8 = (a.C % 8 == 0) && (a.ldy % 8 == 0) && (a.ldo % 8 == 0) &&
             (!a.res || a.ldres % 8 == 0) && (!a.y2 || a.ldy2 % 8 == 0) &&
             (((uintptr_t)a.out) % 16 == 0);
-  if (v8) hipLaunchKernelGGL((bn_apply8_kernel<T, TO>), grid8(a.M, a.C), dim3(256), 0, s, a);
+  if (v8) {
+    const int res = a.y2 ? RES_BN2 : (a.res ? (a.rs > 1 ? RES_SUB : RES_PLAIN) : RES_NONE);
+    const dim3 g = grid8(a.M, a.C);
+#define BN_APPLY_CASE(R)                                                                      \
+    if (res == R) {                                                                           \
+      if (a.relu) hipLaunchKernelGGL((bn_apply8_kernel<T, TO, R, 1>), g, dim3(256), 0, s, a); \
+      else hipLaunchKernelGGL((bn_apply8_kernel<T, TO, R, 0>), g, dim3(256), 0, s, a);        \
+    }
+    BN_APPLY_CASE(RES_NONE) BN_APPLY_CASE(RES_PLAIN) BN_APPLY_CASE(RES_SUB) BN_APPLY_CASE(RES_BN2)
+#undef BN_APPLY_CASE
+  }
   else hipLaunchKernelGGL((bn_apply_kernel<T, TO, 1>), dim3(grid_for(a.M * a.C)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
@@ -510,8 +567,11 @@ template <typename T, typename TZ>
 hipError_t bwd_reduce_t(const BnBwdArgs& a, hipStream_t s) {
   if (bwd_v8<T, TZ>(a)) {
     const int cg_n = a.C / 8;
-    hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ>), dim3(a.rb, cg_n > 256 ? ceil_div(cg_n, 256) : 1),
-                       dim3(256), 0, s, a);
+    const dim3 g(a.rb, cg_n > 256 ? ceil_div(cg_n, 256) : 1);
+    if (a.z && a.dzscale) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 1, 1>), g, dim3(256), 0, s, a);
+    else if (a.z) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 1, 0>), g, dim3(256), 0, s, a);
+    else if (a.dzscale) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 0, 1>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 0, 0>), g, dim3(256), 0, s, a);
   }
   else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, TZ, 1>), dim3(a.rb), dim3(256), 0, s, a);
   return hipGetLastError();
@@ -519,7 +579,20 @@ hipError_t bwd_reduce_t(const BnBwdArgs& a, hipStream_t s) {
 
 template <typename T, typename TZ>
 hipError_t bwd_apply_t(const BnBwdArgs& a, hipStream_t s) {
-  if (bwd_v8<T, TZ>(a)) hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ>), grid8(a.M, a.C), dim3(256), 0, s, a);
+  if (bwd_v8<T, TZ>(a)) {
+    const dim3 g = grid8(a.M, a.C);
+    const int key = (a.z ? 4 : 0) | (a.dzscale ? 2 : 0) | (a.dyhat ? 1 : 0);
+    switch (key) {
+      case 0: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 0, 0, 0>), g, dim3(256), 0, s, a); break;
+      case 1: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 0, 0, 1>), g, dim3(256), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 0, 1, 0>), g, dim3(256), 0, s, a); break;
+      case 3: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 0, 1, 1>), g, dim3(256), 0, s, a); break;
+      case 4: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 1, 0, 0>), g, dim3(256), 0, s, a); break;
+      case 5: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 1, 0, 1>), g, dim3(256), 0, s, a); break;
+      case 6: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 1, 1, 0>), g, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 1, 1, 1>), g, dim3(256), 0, s, a); break;
+    }
+  }
   else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, TZ, 1>), dim3(grid_for(a.M * a.C)), dim3(256), 0, s, a);
   return hipGetLastError();
 }

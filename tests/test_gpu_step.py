@@ -10,8 +10,8 @@ Parameter GRADIENTS at these test sizes are ill-conditioned: BN over a few hundr
 the oracle restated in float32 itself differs from float64 by up to ~3 % on many BN-adjacent
 gradients (tools/diag_step.py prints the table). A gradient tensor is "well conditioned"
 when that fp32-oracle error is < 1e-3; those are held to max(1e-3, 4 x that error). The
-ill-conditioned ones are held to 5e-2 (same order as an fp32 CPU implementation of the
-reference semantics).
+ill-conditioned ones are held to max(5e-2, 2 x that error) (same order as an fp32 CPU
+implementation of the reference semantics; R101 at 48x64 has fp32-oracle gaps up to ~7 %).
 bf16 mode is held to 5e-2 on losses/logits (bf16 storage, fp32 accumulation)."""
 import numpy as np
 import pytest
@@ -90,19 +90,21 @@ def test_train_step_fp32(cuda, cfg):
         for a, b in zip(nat["losses"][4:7], L["counts"]):
             assert abs(int(a) - b) <= max(2, 1e-3 * b)
     assert abs(nat["reg"] - float(L["regularization"])) <= 1e-3 * float(L["regularization"])
-    # low-res logits
+    # low-res logits: 1e-3, or 4x the oracle's own fp32-vs-fp64 gap where the network's
+    # depth amplifies fp32 rounding beyond that (R101: the fp32 oracle itself is 1.8e-3 off)
+    _, low32, g32, _ = _oracle_step(cfg, params, data, dtype=torch.float32)
     c1, c2, c3 = 14, 7, 3
     lg = nat["logits"]
     for key, a, b in (("l1_logits", 0, c1), ("l2_vehicle_logits", c1, c1 + c2),
                       ("l2_human_logits", c1 + c2, c1 + c2 + c3)):
         refl = low[key].detach().permute(0, 2, 3, 1).numpy()
-        assert _rel(lg[..., a:b], refl) < 1e-3, key
+        gap = _rel(low32[key].detach().permute(0, 2, 3, 1).numpy(), refl)
+        assert _rel(lg[..., a:b], refl) < max(1e-3, 4 * gap), (key, gap)
     # gradients of every trainable tensor, conditioning-aware (see module docstring)
-    _, _, g32, _ = _oracle_step(cfg, params, data, dtype=torch.float32)
     errs = {k: _rel(nat["grads"][k], g[k].numpy().reshape(-1)) for k in g}
     cond = {k: _rel(g32[k].numpy().reshape(-1), g[k].numpy().reshape(-1)) for k in g}
     bad = [(errs[k], cond[k], k) for k in g
-           if errs[k] > (max(1e-3, 4 * cond[k]) if cond[k] < 1e-3 else 5e-2)]
+           if errs[k] > (max(1e-3, 4 * cond[k]) if cond[k] < 1e-3 else max(5e-2, 2 * cond[k]))]
     assert not bad, sorted(bad, reverse=True)[:10]
     # SGDM + L2 arithmetic on the native gradients (momentum starts at 0):
     #   w' = w - lr * (g + wd * w)   (wd on conv weights only)
@@ -203,3 +205,67 @@ def test_two_step_fp32(cuda):
         w1 = p1[k].astype(np.float64)
         v2 = 0.9 * v1[k].astype(np.float64) + g2[k].astype(np.float64) + wd * w1
         assert _rel(p2[k], w1 - lr * v2) < 1e-5, k
+
+
+def _bn_bwd_ref(dz, y, z, gamma, eps=1.001e-5):
+    """fp64 BN backward (TF fused training semantics) of relu(bn(y)) given dz, the gradient
+    w.r.t. the relu output z: dy = g*invstd*(dh - mean(dh) - xh*mean(dh*xh)), dh = dz*[z>0]."""
+    y2 = y.reshape(-1, y.shape[-1])
+    dh = (dz * (z > 0)).reshape(y2.shape)
+    mu = y2.mean(0)
+    inv = 1.0 / np.sqrt(y2.var(0) + eps)
+    xh = (y2 - mu) * inv
+    dy = gamma * inv * (dh - dh.mean(0) - xh * (dh * xh).mean(0))
+    return dy.reshape(y.shape)
+
+
+def test_bf16_backward_layerwise(cuda):
+    """bf16 backward, unit by unit, on the tensors the native step itself produced: for each
+    bottleneck, the data gradient of conv3 / conv2 (v2 dgrad) feeding the fused ReLU-mask +
+    BN-backward epilogue must give conv2 / conv1's dy, and every conv's weight gradient must
+    match an fp64 wgrad of the native (bf16) dy and input. Tolerance 2e-2 (bf16 operands,
+    fp32 accumulation; the reference is fed the same bf16 tensors)."""
+    from input_pipelines.synthetic import batch
+    from oracle.tfseg import build_specs, conv_tf
+    from seg_hip import SegContext
+    cfg = SegConfig(height=64, width=128, nb_pp=2, pyramid="psp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=7).items()}
+    data = batch(13, cfg.nb_pp, 0, 0, cfg.height, cfg.width)
+    ctx = SegContext(pyramid="psp", height=64, width=128, nb_pp=2, dtype="bf16")
+    ctx.load_params(params)
+    ctx.forward(torch.as_tensor(data["images"]).to(cuda))
+    ctx.loss(torch.as_tensor(data["px"]).to(cuda))
+    ctx.backward()
+    torch.cuda.synchronize()
+    grads = ctx.named("grads")
+    specs = build_specs(cfg)
+    idx = {s.name: i for i, s in enumerate(specs)}
+    T = lambda a: torch.as_tensor(a, dtype=torch.float64).permute(0, 3, 1, 2)
+    wbf = lambda n: torch.as_tensor(params[n + "/weights"]).to(torch.bfloat16).double()
+    checked = 0
+    for s in specs:
+        unit = s.name[:-len("/conv1")]
+        if not s.name.endswith("/conv1") or f"{unit}/conv2" not in idx:
+            continue
+        for up, lo in (("conv3", "conv2"), ("conv2", "conv1")):
+            su, sl = specs[idx[f"{unit}/{up}"]], specs[idx[f"{unit}/{lo}"]]
+            dyu = ctx.debug_tensor(f"conv{idx[su.name]}_dy")
+            xu = T(ctx.debug_tensor(f"conv{idx[su.name]}_x")).requires_grad_(True)
+            conv_tf(xu, wbf(su.name), su).backward(T(dyu))
+            dz = xu.grad.permute(0, 2, 3, 1).numpy()
+            yl = ctx.debug_tensor(f"conv{idx[sl.name]}_y").astype(np.float64)
+            zl = ctx.debug_tensor(f"conv{idx[su.name]}_x").astype(np.float64)
+            gamma = params[sl.name + "/BatchNorm/gamma"].astype(np.float64)
+            ref = _bn_bwd_ref(dz, yl, zl, gamma)
+            got = ctx.debug_tensor(f"conv{idx[sl.name]}_dy")
+            assert _rel(got, ref) < 2e-2, (sl.name, _rel(got, ref))
+        for name in ("conv1", "conv2", "conv3"):
+            sp = specs[idx[f"{unit}/{name}"]]
+            i = idx[sp.name]
+            w = wbf(sp.name).requires_grad_(True)
+            conv_tf(T(ctx.debug_tensor(f"conv{i}_x")), w, sp).backward(T(ctx.debug_tensor(f"conv{i}_dy")))
+            ref = w.grad.numpy().reshape(-1)
+            assert _rel(grads[sp.name + "/weights"], ref) < 2e-2, (sp.name, _rel(grads[sp.name + "/weights"], ref))
+        checked += 1
+    assert checked == 16 + 3   # R50 units + adaptation bottlenecks
+    ctx.close()
