@@ -26,12 +26,6 @@ struct ConvArgs {
   int st;         // transposed stride: src valid iff divisible by st (1 = plain conv)
   int pad_h, pad_w, dil;
   float* stats;   // BN partials [mtiles][Co] x {sum, M2} (nullptr = none)
-  // fused batch-norm backward reduce (v2 dgrad only, bnpart != nullptr): the output is the
-  // gradient w.r.t. relu(bn(bny)); the epilogue masks it by recomputing bn(bny) > 0, stores
-  // the masked gradient and writes per-256-row partials {sum dyhat, sum dyhat*xhat}
-  const void* bny; int ldbny;
-  const float* bnmu; const float* bnsc; const float* bnbe; const float* bninv;
-  float* bnpart;  // [mtiles][Co][2]
 };
 
 struct WgradArgs {
@@ -56,7 +50,7 @@ int conv_nt_mtiles(long M);  // upper bound on BN-stat partial tiles (128-row ti
 // rows per BN-stat partial tile of the kernel launch_conv_nt will pick (128 or 256)
 int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a);
 bool conv_nt_v2_ok(const ConvArgs& a);
-// true when launch_conv_nt runs the v2 kernel (required for stats-free fused BN epilogues)
+// true when launch_conv_nt runs the v2 kernel
 bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a);
 hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s);
 bool conv_wgrad_v2_ok(const WgradArgs& a);

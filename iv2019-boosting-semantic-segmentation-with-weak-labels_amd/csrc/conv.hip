@@ -596,7 +596,6 @@ bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a) {
 
 hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t s) {
   if (conv_nt_uses_v2(dtype, out_f32, a)) return launch_conv_nt_v2(a, s);
-  if (a.bnpart) return hipErrorInvalidValue;   // fused BN epilogue exists on v2 only
   if (dtype == SEG_BF16) {
     if (out_f32) return nt_dispatch<bf16_t, float>(a, s);
     return nt_dispatch<bf16_t, bf16_t>(a, s);

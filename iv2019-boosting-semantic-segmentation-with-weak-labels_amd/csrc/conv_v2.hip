@@ -175,22 +175,6 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
     }
   };
 
-  // fused BN-backward epilogue: the BN layer's y rows this thread will need, fetched during
-  // the last K-step (no DMA is in flight then) so the epilogue does not wait on HBM
-  const int s_rl = tid >> 3, s_cc = tid & 7;   // store phase: row lane (0..63), 8-col chunk
-  const bf16_t* BY = (const bf16_t*)a.bny;
-  // (pass 0's rows during the last K-step, pass p+1's rows at the start of pass p)
-  uint4 ycur[BM / 64], ynext[BM / 64];
-  auto prefetch_y = [&](int ps, uint4 (&dst)[BM / 64]) {
-#pragma unroll
-    for (int rr = 0; rr < BM / 64; ++rr) {
-      const long m = m0 + s_rl + 64 * rr;
-      const int n = n0 + ps * EPI_COLS + s_cc * 8;
-      dst[rr] = (m < M && n < a.Co) ? *(const uint4*)(BY + (size_t)m * a.ldbny + n)
-                                    : make_uint4(0, 0, 0, 0);
-    }
-  };
-
   // ---- main loop: STAGES-deep LDS ring filled by LDS-DMA ----
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -205,7 +189,6 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
     }
     __builtin_amdgcn_s_barrier();   // every lane's DMA for kb landed; stage (kb-1) is free
     if (kb + STAGES - 1 < nk) issue(kb + STAGES - 1, (kb + STAGES - 1) % STAGES);
-    if (BY && kb == nk - 1) prefetch_y(0, ycur);
     compute(kb % STAGES);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -285,11 +268,10 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   bf16_t* Y = (bf16_t*)a.y;
   const bf16_t* R1 = (const bf16_t*)a.r;
   const bf16_t* R2 = (const bf16_t*)a.r2;
-  float* bred = (float*)(smem + BM * EPI_LD * 4);   // [64][64 cols][2] fused-BN partials
+  const int s_rl = tid >> 3, s_cc = tid & 7;   // store phase: row lane (0..63), 8-col chunk
 #pragma unroll
   for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
     const int cbase = pass * EPI_COLS;
-    if (BY && pass + 1 < BN / EPI_COLS) prefetch_y(pass + 1, ynext);
     if (wn * WN + WN > cbase && wn * WN < cbase + EPI_COLS) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -305,15 +287,6 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
     }
     __syncthreads();
     const int n = n0 + cbase + s_cc * 8;
-    float b1[8], b2[8], bmu[8], bsc[8], bbe[8], binv[8];
-    if (BY) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        b1[e] = 0.f; b2[e] = 0.f;
-        const int c = n < a.Co ? n + e : 0;
-        bmu[e] = a.bnmu[c]; bsc[e] = a.bnsc[c]; bbe[e] = a.bnbe[c]; binv[e] = a.bninv[c];
-      }
-    }
     if (n < a.Co) {   // Co % 8 == 0 on this path
 #pragma unroll
       for (int rr = 0; rr < BM / 64; ++rr) {
@@ -335,45 +308,9 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += u[e];
           }
-          if (BY) {
-            // gradient w.r.t. bn output gated by relu(bn(y)) > 0 (same fp32 expression as
-            // bn_apply8), rounded as stored, then this row's share of the BN-backward sums
-            float yv[8];
-            {
-              const uint4 u = ycur[rr];
-              const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-              for (int q = 0; q < 4; ++q) { yv[2 * q] = bf2f((bf16_t)(w4[q] & 0xffff)); yv[2 * q + 1] = bf2f((bf16_t)(w4[q] >> 16)); }
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float zb = __builtin_fmaf(yv[e] - bmu[e], bsc[e], bbe[e]);
-              const float d = zb > 0.f ? bf2f(f2bf(v[e])) : 0.f;
-              v[e] = d;
-              b1[e] += d;
-              b2[e] += d * ((yv[e] - bmu[e]) * binv[e]);
-            }
-          }
           Vec8<bf16_t>::store(Y + (size_t)m * a.ldy + n, v);
         }
       }
-    }
-    if (BY) {
-      // rows of this tile: each thread's 4-row partials -> LDS [64 row lanes][64 cols][2],
-      // then 128 threads sum one (column, quantity) over the 64 row lanes in fixed order
-#pragma unroll
-      for (int e = 0; e < 8; e += 2)   // 64 contiguous bytes per thread: ds_write_b128 x 4
-        *(float4*)(bred + (s_rl * 64 + s_cc * 8 + e) * 2) = make_float4(b1[e], b2[e], b1[e + 1], b2[e + 1]);
-      __syncthreads();
-      if (tid < 128) {
-        float t = 0.f;
-#pragma unroll 16
-        for (int r = 0; r < 64; ++r) t += bred[r * 128 + tid];
-        const int col = tid >> 1;
-        if (n0 + cbase + col < a.Co) a.bnpart[2 * ((size_t)mt * a.Co + n0 + cbase + col) + (tid & 1)] = t;
-      }
-#pragma unroll
-      for (int rr = 0; rr < BM / 64; ++rr) ycur[rr] = ynext[rr];
     }
     __syncthreads();
   }
@@ -383,7 +320,7 @@ template <int BN, int WMW, int WNW, int STAGES, int ST>
 hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 256;
   constexpr int STAGE_BYTES = (BM + BN) * 128;
-  constexpr int EPI = BM * (64 + 4) * 4 + 64 * 64 * 2 * 4;   // staging + fused-BN partials
+  constexpr int EPI = BM * (64 + 4) * 4 + 64 * 8 * 8 * 4;
   constexpr int LDS = STAGES * STAGE_BYTES > EPI ? STAGES * STAGE_BYTES : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST>;
@@ -443,7 +380,7 @@ __device__ __forceinline__ int wswz(int row, int ch) {
   else return ch ^ (2 * (row & 3));
 }
 
-template <int BM, int BN, int WMW, int WNW>
+template <int BM, int BN, int WMW, int WNW, int STAGES>
 __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs a) {
   constexpr int ROWB_A = BM * 2, ROWB_B = BN * 2;            // bytes per pixel row
   constexpr int CPR_A = BM / 8, CPR_B = BN / 8;              // 16-B chunks per row
@@ -453,7 +390,6 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   constexpr int LPK = AI + BI;
   constexpr int A_BYTES = WBK * ROWB_A, B_BYTES = WBK * ROWB_B;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int STAGES = 3;
   constexpr int WM = BM / WMW, WN = BN / WNW;
   constexpr int FM = WM / 16, FN = WN / 16;
   static_assert(WMW * WNW == 8, "8 waves");
@@ -580,8 +516,12 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s, s);
   for (int kb = 0; kb < nk; ++kb) {
-    if (kb + 1 < nk) wait_vmcnt<LPK>();
-    else wait_vmcnt<0>();
+    if constexpr (STAGES == 3) {
+      if (kb + 1 < nk) wait_vmcnt<LPK>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
     __builtin_amdgcn_s_barrier();
     if (kb + STAGES - 1 < nk) issue(kb + STAGES - 1, (kb + STAGES - 1) % STAGES);
     compute(kb % STAGES);
@@ -603,11 +543,11 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
     }
 }
 
-template <int BM, int BN, int WMW, int WNW>
+template <int BM, int BN, int WMW, int WNW, int STAGES>
 hipError_t wg2_launch(const WgradArgs& a, hipStream_t s) {
-  constexpr int LDS = 3 * WBK * (BM + BN) * 2;
+  constexpr int LDS = STAGES * WBK * (BM + BN) * 2;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_wgrad_v2_kernel<BM, BN, WMW, WNW>;
+  auto kern = conv_wgrad_v2_kernel<BM, BN, WMW, WNW, STAGES>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -627,9 +567,10 @@ bool conv_wgrad_v2_ok(const WgradArgs& a) {
          (long)a.N * a.Ho * a.Wo < (1L << 31);
 }
 
-// tile (BM co x BN cols) chosen so that the per-split work covers the co / column extents
+// tile (BM co x BN cols): the largest the extents fill. 256 x 256 (wave tiles 128 x 64) keeps
+// LDS fragment traffic below the MFMA time and halves L2 re-reads vs 128 x 256.
 void conv_wgrad_v2_tile(int Co, int Ncol, int* bm, int* bn) {
-  *bm = Co <= 64 ? 64 : 128;
+  *bm = Co <= 64 ? 64 : (Co <= 128 ? 128 : 256);
   *bn = Ncol <= 64 ? 64 : (Ncol <= 128 ? 128 : 256);
 }
 
@@ -637,11 +578,16 @@ hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s) {
   int bm, bn;
   conv_wgrad_v2_tile(a.Co, a.KH * a.KW * a.C, &bm, &bn);
   if (bm == 64) {
-    if (bn == 64) return wg2_launch<64, 64, 4, 2>(a, s);
-    if (bn == 128) return wg2_launch<64, 128, 2, 4>(a, s);
-    return wg2_launch<64, 256, 2, 4>(a, s);
+    if (bn == 64) return wg2_launch<64, 64, 4, 2, 3>(a, s);
+    if (bn == 128) return wg2_launch<64, 128, 2, 4, 3>(a, s);
+    return wg2_launch<64, 256, 2, 4, 3>(a, s);
   }
-  if (bn == 64) return wg2_launch<128, 64, 4, 2>(a, s);
-  if (bn == 128) return wg2_launch<128, 128, 4, 2>(a, s);
-  return wg2_launch<128, 256, 2, 4>(a, s);
+  if (bm == 128) {
+    if (bn == 64) return wg2_launch<128, 64, 4, 2, 3>(a, s);
+    if (bn == 128) return wg2_launch<128, 128, 4, 2, 3>(a, s);
+    return wg2_launch<128, 256, 2, 4, 3>(a, s);
+  }
+  if (bn == 64) return wg2_launch<256, 64, 8, 1, 3>(a, s);
+  if (bn == 128) return wg2_launch<256, 128, 4, 2, 3>(a, s);
+  return wg2_launch<256, 256, 2, 4, 2>(a, s);
 }

@@ -319,8 +319,7 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
   long M = (long)N * L.Ho * L.Wo;
   if (int r = dalloc(c, &L.stats_part, (size_t)conv_nt_mtiles(M) * L.co * 2)) return r;
   L.rb = bn_bwd_rowblocks(M, L.co);
-  // row blocks of the BN-backward reduce, or 256-row tiles of a fused dgrad epilogue
-  if (int r = dalloc(c, &L.bwd_part, (size_t)std::max<long>(L.rb, ceil_div(M, 256)) * L.co * 2)) return r;
+  if (int r = dalloc(c, &L.bwd_part, (size_t)L.rb * L.co * 2)) return r;
   size_t need = (size_t)((conv_nt_mtiles(M) + 63) / 64) * L.co * 3;
   c->stat_scratch_floats = std::max(c->stat_scratch_floats, need);
   return 0;
@@ -413,10 +412,8 @@ int bn_apply(Step& S, int li, const Act& out, int out_f32, const Act* res = null
 }
 
 // BN backward for layer li: dz (gradient wrt BN output), z (mask source or null)
-// fused_rows > 0: dz already holds the masked gradient and bwd_part the per-tile partial
-// sums written by the producing dgrad's epilogue (tiles of fused_rows rows)
 int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const Act* dyhat_out,
-                const float* dzscale = nullptr, int fused_rows = 0) {
+                const float* dzscale = nullptr) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
   BnBwdArgs a{};
@@ -433,31 +430,21 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   const double me = a.M * (double)a.C * 1e-9;
   const double gb_in = me * (zsz * (z ? 2 : 1) + esz);
   int slot;
-  int nparts = L.rb;
-  if (fused_rows > 0) {
-    a.z = nullptr; a.ldz = 0;
-    nparts = (int)ceil_div(a.M, fused_rows);
-  } else {
-    if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
-    HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
-    if (int r = prof_end(c, S.s, slot)) return r;
-  }
+  if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
+  HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
   const bool tb = c->cfg.train_bn != 0;
-  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, nparts, a.M, L.co, L.st,
+  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
                                     tb ? c->grads + L.g_off : nullptr,
                                     tb ? c->grads + L.b_off : nullptr, S.s));
-  const double gb_apply = fused_rows > 0 ? me * (zsz + 2 * esz) : gb_in + me * esz * (dyhat_out ? 2 : 1);
+  const double gb_apply = gb_in + me * esz * (dyhat_out ? 2 : 1);
   if (int r = prof_begin(c, S.s, 5, li, gb_apply, &slot)) return r;
   HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
   return prof_end(c, S.s, slot);
 }
 
 // dx = dgrad(dy) [+ r1] [+ r2]
-// bn_li >= 0: dx is the gradient w.r.t. relu(bn(conv bn_li)); when the v2 kernel runs, its
-// epilogue applies the ReLU mask and writes bn_li's BN-backward partials. *fused_rows gets the
-// partial tile height (0 = not fused: the caller runs the separate reduce).
-int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr,
-               int bn_li = -1, int* fused_rows = nullptr) {
+int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
   ConvArgs a{};
@@ -471,14 +458,6 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
   a.sf = 1; a.st = L.stride;
   a.pad_h = (keff - 1) - L.pad_h; a.pad_w = (keff - 1) - L.pad_w;
   a.dil = L.rate; a.stats = nullptr;
-  if (fused_rows) *fused_rows = 0;
-  if (bn_li >= 0 && conv_nt_uses_v2(S.dt, 0, a)) {
-    ConvL& B = c->convs[bn_li];
-    a.bny = B.y.p; a.ldbny = B.y.ld;
-    a.bnmu = B.st.mean; a.bnsc = B.st.scale; a.bnbe = c->params + B.b_off; a.bninv = B.st.invstd;
-    a.bnpart = B.bwd_part;
-    if (fused_rows) *fused_rows = 256;
-  }
   long M = (long)L.N * L.H * L.W;
   int slot;
   if (int r = prof_begin(c, S.s, 1, li, 2.0 * M * L.ci * L.k * L.k * L.co * 1e-9 / L.stride / L.stride, &slot)) return r;
@@ -763,13 +742,12 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
   if (int r = bn_backward(S, u.c3, u.dout, 0, &u.out, dpre)) return r;
   if (u.kind == SC_CONV)
     if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
-  int fr = 0;
   if (int r = conv_wgrad(S, u.c3, u.z2)) return r;
-  if (int r = conv_dgrad(S, u.c3, u.dz2, nullptr, nullptr, u.c2, &fr)) return r;
-  if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr, nullptr, fr)) return r;
+  if (int r = conv_dgrad(S, u.c3, u.dz2)) return r;
+  if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr)) return r;
   if (int r = conv_wgrad(S, u.c2, u.z1)) return r;
-  if (int r = conv_dgrad(S, u.c2, u.dz1, nullptr, nullptr, u.c1, &fr)) return r;
-  if (int r = bn_backward(S, u.c1, u.dz1, 0, &u.z1, nullptr, nullptr, fr)) return r;
+  if (int r = conv_dgrad(S, u.c2, u.dz1)) return r;
+  if (int r = bn_backward(S, u.c1, u.dz1, 0, &u.z1, nullptr)) return r;
   if (int r = conv_wgrad(S, u.c1, u.in)) return r;
   switch (u.kind) {
     case SC_IDENTITY:
