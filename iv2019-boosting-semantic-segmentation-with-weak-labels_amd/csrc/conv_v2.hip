@@ -15,6 +15,10 @@
 //    mean) for the fused batch-norm.
 #include "conv.h"
 
+#ifndef SEG_MFMA_PRIO
+#define SEG_MFMA_PRIO 1   // s_setprio(1) around MFMA clusters (+1-2 % measured)
+#endif
+
 // 16-byte zero source for out-of-bounds (padding) taps of the LDS-DMA gather
 __device__ __attribute__((aligned(64))) bf16_t g_zero16[64];
 
@@ -111,14 +115,13 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
     a_w0[i] = wo * a.sf - a.pad_w;
   }
 
-  auto issue = [&](int kb, int stage) {
+  auto issue_a = [&](int kb, int stage) {
     const int k0 = kb * BK;
     const int tap = k0 / a.C;
     const int c0 = k0 - tap * a.C;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     const int dh = kh * a.dil, dw = kw * a.dil;
     char* sA = smem + stage * STAGE_BYTES;
-    char* sB = sA + BM * 128;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int lc = swz(a_row[i], pc);
@@ -135,6 +138,10 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
       const size_t off = ((size_t)(a_nb[i] + hi) * a.W + wi) * a.ldx + c0 + lc * 8;
       glds16(ok ? (const void*)(X + off) : (const void*)zero, sA + (i * 8 + wave) * 1024);
     }
+  };
+  auto issue_b = [&](int kb, int stage) {
+    const int k0 = kb * BK;
+    char* sB = smem + stage * STAGE_BYTES + BM * 128;
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int row = (i * 8 + wave) * 8 + (lane >> 3);
@@ -151,11 +158,17 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int stage) {
+  // one K-step of MFMAs; the next stage's LDS-DMA is issued in two parts, one ahead of each
+  // 32-deep k-substep, so its issue cost spreads over the MFMA stream
+  auto compute = [&](int stage, int nkb, int nstage) {
     const char* A = smem + stage * STAGE_BYTES;
     const char* B = A + BM * 128;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+      if (nkb >= 0) {
+        if (s == 0) issue_a(nkb, nstage);
+        else issue_b(nkb, nstage);
+      }
       bf16x8_t af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
@@ -167,18 +180,24 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
         const int row = wn * WN + j * 16 + lr;
         bfr[j] = *(const bf16x8_t*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
       }
+#if SEG_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#if SEG_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
   };
 
   // ---- main loop: STAGES-deep LDS ring filled by LDS-DMA ----
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s, s);
+    if (s < nk) { issue_a(s, s); issue_b(s, s); }
   for (int kb = 0; kb < nk; ++kb) {
     // K-step kb has landed for this lane once at most (issued later) steps remain in flight
     if constexpr (STAGES == 3) {
@@ -188,8 +207,8 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
       wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();   // every lane's DMA for kb landed; stage (kb-1) is free
-    if (kb + STAGES - 1 < nk) issue(kb + STAGES - 1, (kb + STAGES - 1) % STAGES);
-    compute(kb % STAGES);
+    const int nkb = kb + STAGES - 1 < nk ? kb + STAGES - 1 : -1;
+    compute(kb % STAGES, nkb, (kb + STAGES - 1) % STAGES);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -197,8 +216,64 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   // ---- epilogue ----
   const int rows_valid = (int)((M - m0) < BM ? (M - m0) : BM);
   float* red = (float*)smem;          // [WMW][BN] column partials
-  if (a.stats) {
-    // BN statistics straight from the accumulators (values rounded as stored):
+  if (a.stats && rows_valid == BM) {
+    // full tile, one pass over the accumulators: per lane and column, (sum, M2) of its 4*FM
+    // rows from (sum, sum of squares); then Chan merges of equal-count groups over the lane
+    // groups (shfl 16, 32) and the WMW waves (LDS), fixed order
+    float2* red2 = (float2*)smem;     // [WMW][BN] (sum, M2)
+    constexpr float NL = 4.f * FM;    // rows per lane
+    float sj[FN], mj[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = acc[i][j][r];
+          sm += x;
+          sq = __builtin_fmaf(x, x, sq);
+        }
+      sj[j] = sm;
+      mj[j] = fmaxf(sq - sm * sm * (1.f / NL), 0.f);
+    }
+    float n = NL;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
+        const float d = (s2 - sj[j]) / n;
+        mj[j] = mj[j] + m2 + d * d * (0.5f * n);
+        sj[j] += s2;
+      }
+      n *= 2.f;
+    }
+    if (lq == 0)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red2[wm * BN + wn * WN + j * 16 + lr] = make_float2(sj[j], mj[j]);
+    __syncthreads();
+    if (wm == 0 && lq == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * WN + j * 16 + lr;
+        float2 t = red2[c];
+        float nt = (float)WM;
+#pragma unroll
+        for (int w = 1; w < WMW; ++w) {
+          const float2 u = red2[w * BN + c];
+          const float d = u.x / (float)WM - t.x / nt;
+          t.y = t.y + u.y + d * d * (nt * (float)WM / (nt + (float)WM));
+          t.x += u.x;
+          nt += (float)WM;
+        }
+        if (n0 + c < a.Co)   // one (sum, M2) per 256-row tile (conv_nt_stat_rows)
+          *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = t;
+      }
+    }
+    __syncthreads();
+  } else if (a.stats) {
+    // partial tile: two passes with row masks, from the fp32 accumulators:
     // column sums over the wave's rows -> lane groups (shfl) -> the WMW waves (LDS)
     float cs[FN];
 #pragma unroll
@@ -209,7 +284,7 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = wm * WM + i * 16 + lq * 4 + r;
-          const float x = row < rows_valid ? bf2f(f2bf(acc[i][j][r])) : 0.f;
+          const float x = row < rows_valid ? acc[i][j][r] : 0.f;
           v += x;
         }
       v += __shfl_xor(v, 16, 64);
@@ -238,7 +313,7 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = wm * WM + i * 16 + lq * 4 + r;
-          const float d = bf2f(f2bf(acc[i][j][r])) - mean[j];
+          const float d = acc[i][j][r] - mean[j];
           v += row < rows_valid ? d * d : 0.f;
         }
       v += __shfl_xor(v, 16, 64);
@@ -372,7 +447,6 @@ hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s) {
 namespace {
 
 constexpr int WG_THREADS = 512;
-constexpr int WBK = 64;  // pixels per K-step
 
 template <int COLS>
 __device__ __forceinline__ int wswz(int row, int ch) {
@@ -380,7 +454,7 @@ __device__ __forceinline__ int wswz(int row, int ch) {
   else return ch ^ (2 * (row & 3));
 }
 
-template <int BM, int BN, int WMW, int WNW, int STAGES>
+template <int BM, int BN, int WMW, int WNW, int STAGES, int WBK>
 __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs a) {
   constexpr int ROWB_A = BM * 2, ROWB_B = BN * 2;            // bytes per pixel row
   constexpr int CPR_A = BM / 8, CPR_B = BN / 8;              // 16-B chunks per row
@@ -399,12 +473,23 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WNW, wn = wave % WNW;
-  const int m0 = blockIdx.x * BM;   // co
-  const int n0 = blockIdx.y * BN;   // (tap, ci)
   const int Ncol = a.KH * a.KW * a.C;
   const int P = a.N * a.Ho * a.Wo;
+  // XCD-aware bijective remap of the 1-D grid: workgroups are dealt round-robin over the 8
+  // XCDs; give each XCD a contiguous run of (split-major, co fastest) tiles so all tiles of a
+  // pixel split share one L2 (dy rows reused across column tiles, x rows across co tiles)
+  const int mtn = (a.Co + BM - 1) / BM, ntn = (Ncol + BN - 1) / BN;
+  const int nwg = mtn * ntn * a.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = wg / (mtn * ntn);
+  const int rem = wg - split * mtn * ntn;
+  const int nt_ = rem / mtn, mt_ = rem - nt_ * mtn;
+  const int m0 = mt_ * BM;   // co
+  const int n0 = nt_ * BN;   // (tap, ci)
   const int chunk = ((P + a.splits - 1) / a.splits + WBK - 1) / WBK * WBK;
-  const int p_begin = blockIdx.z * chunk;
+  const int p_begin = split * chunk;
   const int p_end = (p_begin + chunk < P) ? p_begin + chunk : P;
   const int nk = p_end > p_begin ? (p_end - p_begin + WBK - 1) / WBK : 0;
   const bf16_t* DY = (const bf16_t*)a.dy;
@@ -487,7 +572,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
     const char* A = smem + stg * STAGE;
     const char* B = A + A_BYTES;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {     // two 32-pixel MFMA k-steps per stage
+    for (int s = 0; s < WBK / 32; ++s) {     // 32-pixel MFMA k-steps per stage
       const int kr = 32 * s + 8 * lq + q4;
       bf16x8_t af[FM], bfr[FN];
 #pragma unroll
@@ -504,11 +589,17 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
         short t8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         __builtin_memcpy(&bfr[j], t8, 16);
       }
+#if SEG_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#if SEG_MFMA_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
   };
 
@@ -516,8 +607,14 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s, s);
   for (int kb = 0; kb < nk; ++kb) {
-    if constexpr (STAGES == 3) {
-      if (kb + 1 < nk) wait_vmcnt<LPK>();
+    // K-step kb has landed once only the (already issued) later steps remain in flight
+    const int later = min(STAGES - 2, nk - 1 - kb);
+    if constexpr (STAGES >= 4) {
+      if (later >= 2) wait_vmcnt<2 * LPK>();
+      else if (later == 1) wait_vmcnt<LPK>();
+      else wait_vmcnt<0>();
+    } else if constexpr (STAGES == 3) {
+      if (later >= 1) wait_vmcnt<LPK>();
       else wait_vmcnt<0>();
     } else {
       wait_vmcnt<0>();
@@ -528,7 +625,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  float* O = a.out + (size_t)blockIdx.z * a.Co * Ncol;
+  float* O = a.out + (size_t)split * a.Co * Ncol;
   const int lr = lane & 15;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -543,11 +640,12 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
     }
 }
 
-template <int BM, int BN, int WMW, int WNW, int STAGES>
+template <int BM, int BN, int WMW, int WNW, int STAGES, int WBK = 64>
 hipError_t wg2_launch(const WgradArgs& a, hipStream_t s) {
   constexpr int LDS = STAGES * WBK * (BM + BN) * 2;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_wgrad_v2_kernel<BM, BN, WMW, WNW, STAGES>;
+  static_assert(STAGES <= 4 && (STAGES < 4 || 2 * (WBK * (BM + BN) / 8 / WG_THREADS) <= 16), "vmcnt");
+  auto kern = conv_wgrad_v2_kernel<BM, BN, WMW, WNW, STAGES, WBK>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -555,8 +653,8 @@ hipError_t wg2_launch(const WgradArgs& a, hipStream_t s) {
     attr = true;
   }
   const int Ncol = a.KH * a.KW * a.C;
-  dim3 grid(ceil_div(a.Co, BM), ceil_div(Ncol, BN), a.splits);
-  hipLaunchKernelGGL(kern, grid, dim3(WG_THREADS), LDS, s, a);
+  const int nwg = ceil_div(a.Co, BM) * ceil_div(Ncol, BN) * a.splits;
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(WG_THREADS), LDS, s, a);
   return hipGetLastError();
 }
 

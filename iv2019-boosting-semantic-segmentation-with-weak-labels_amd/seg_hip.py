@@ -15,7 +15,8 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libseg_hip.so")
+# SEG_HIP_LIB: development override (kernel A/B variants built by `make VARIANT=...`)
+LIB_PATH = os.environ.get("SEG_HIP_LIB") or os.path.join(_HERE, "libseg_hip.so")
 
 EXPORTED_SYMBOLS = [
     "seg_create", "seg_destroy", "seg_last_error", "seg_sizes", "seg_bind_buffers",

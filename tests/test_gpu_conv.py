@@ -85,8 +85,12 @@ def test_conv_fwd(cuda, dtype, case):
     mean = st[:, :, 0].sum(0) / M
     tile_mean = st[:, :, 0] / cnt[:, None]
     m2 = st[:, :, 1].sum(0) + (cnt[:, None] * (tile_mean - mean) ** 2).sum(0)
-    yr = y.reshape(-1, Co).astype(np.float64)
-    assert _rel(mean, yr.mean(0)) < 1e-4
+    # fp32: against the stored output; bf16: the statistics are taken from the fp32
+    # accumulators (before the bf16 rounding of the stored y), so against the fp64 reference
+    # (mean error measured in units of the channel's standard deviation: means are ~0 here)
+    yr = (y if dtype == "fp32" else ref).reshape(-1, Co).astype(np.float64)
+    sd = np.sqrt(yr.var(0))
+    assert np.linalg.norm(mean - yr.mean(0)) / np.linalg.norm(sd) < (1e-5 if dtype == "fp32" else 1e-3)
     assert _rel(m2 / M, yr.var(0)) < 1e-3
 
 
