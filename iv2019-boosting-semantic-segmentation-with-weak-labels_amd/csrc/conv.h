@@ -26,6 +26,8 @@ struct ConvArgs {
   int st;         // transposed stride: src valid iff divisible by st (1 = plain conv)
   int pad_h, pad_w, dil;
   float* stats;   // BN partials [mtiles][Co] x {sum, M2} (nullptr = none)
+  int tap8;       // 1: C == 8 and every 16-B chunk of K is one tap (the 3-channel stem padded
+                  // to 8); K = KH*KW*8 is padded to a multiple of 64 with zero weights
 };
 
 struct WgradArgs {
@@ -56,3 +58,13 @@ hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s);
 bool conv_wgrad_v2_ok(const WgradArgs& a);
 hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s);
 void conv_wgrad_v2_tile(int Co, int Ncol, int* bm, int* bn);
+
+// 3-channel stem in bf16, laid out as 8-channel taps (tap8 mode):
+//   images f32 [M][3] -> bf16 [M][8] (channels 3..7 zero)
+hipError_t launch_cast_pad8(const float* src, bf16_t* dst, long M, hipStream_t s);
+//   weights bf16 [Co][taps][ci] -> [Co][ldw] with 8-channel taps, zero padded
+hipError_t launch_stem_pad_weights(const bf16_t* w, bf16_t* wp, int co, int taps, int ci, int ldw,
+                                   hipStream_t s);
+//   split-K slabs [splits][co_pad][taps*8] -> fp32 [co][taps][ci] (drops the pad channels)
+hipError_t launch_splitk_reduce_pad8(const float* part, int splits, long split_stride, int co,
+                                     int taps, int ci, float* out, hipStream_t s);

@@ -590,6 +590,56 @@ int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a) {
   return (dtype == SEG_BF16 && !out_f32 && conv_nt_v2_ok(a)) ? 256 : 128;
 }
 
+namespace {
+__global__ void cast_pad8_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst, long M) {
+  for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (long)gridDim.x * blockDim.x) {
+    const float* p = src + 3 * m;
+    const uint32_t w0 = (uint32_t)f2bf(p[0]) | ((uint32_t)f2bf(p[1]) << 16);
+    const uint32_t w1 = (uint32_t)f2bf(p[2]);
+    *(uint4*)(dst + 8 * m) = make_uint4(w0, w1, 0u, 0u);
+  }
+}
+__global__ void stem_pad_weights_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp,
+                                        int co, int taps, int ci, int ldw) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= co * ldw) return;
+  const int o = i / ldw, k = i - o * ldw;
+  const int t = k >> 3, c = k & 7;
+  wp[i] = (t < taps && c < ci) ? w[((size_t)o * taps + t) * ci + c] : (bf16_t)0;
+}
+__global__ void splitk_reduce_pad8_kernel(const float* __restrict__ part, int splits, long stride,
+                                          int co, int taps, int ci, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = co * taps * ci;
+  if (i >= n) return;
+  const int o = i / (taps * ci), r = i - o * taps * ci;
+  const int t = r / ci, c = r - t * ci;
+  const long src = (long)o * taps * 8 + t * 8 + c;
+  float acc = 0.f;
+  for (int z = 0; z < splits; ++z) acc += part[(size_t)z * stride + src];   // fixed order
+  out[i] = acc;
+}
+}  // namespace
+
+hipError_t launch_cast_pad8(const float* src, bf16_t* dst, long M, hipStream_t s) {
+  long g = (M + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(cast_pad8_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, s, src, dst, M);
+  return hipGetLastError();
+}
+hipError_t launch_stem_pad_weights(const bf16_t* w, bf16_t* wp, int co, int taps, int ci, int ldw,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(stem_pad_weights_kernel, dim3(ceil_div((long)co * ldw, 256)), dim3(256), 0, s, w,
+                     wp, co, taps, ci, ldw);
+  return hipGetLastError();
+}
+hipError_t launch_splitk_reduce_pad8(const float* part, int splits, long split_stride, int co,
+                                     int taps, int ci, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(splitk_reduce_pad8_kernel, dim3(ceil_div((long)co * taps * ci, 256)), dim3(256), 0,
+                     s, part, splits, split_stride, co, taps, ci, out);
+  return hipGetLastError();
+}
+
 bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a) {
   return dtype == SEG_BF16 && !out_f32 && conv_nt_v2_ok(a);
 }

@@ -55,8 +55,11 @@ struct OutT;
 template <> struct OutT<0> { typedef bf16_t T; };
 template <> struct OutT<1> { typedef float T; };
 
-// BM = 256; waves laid out WMW (M) x WNW (N)
-template <int BN, int WMW, int WNW, int STAGES, int ST>
+// BM = 256; waves laid out WMW (M) x WNW (N); STAGES-deep ring of 64-deep K-steps.
+// (Measured and rejected: splitting each stage into two 32-deep units refilled one phase
+// after their last read -- 1.5 K-steps of prefetch instead of 1 -- ran 5-8 % slower: the
+// extra barrier per K-step costs more than the deeper prefetch gains.)
+template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0>
 __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   const bf16_t* zero = g_zero16;
   constexpr int BM = 256;
@@ -92,17 +95,19 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   const long m0 = (long)mt * BM;
   const int n0 = nt * BN;
   const int K = a.KH * a.KW * a.C;
-  const int nk = K / BK;
+  const int nk = T8 ? (K + BK - 1) / BK : K / BK;   // T8: taps beyond KH*KW read zeros
   const bf16_t* X = (const bf16_t*)a.x;
   const bf16_t* Wt = (const bf16_t*)a.w;
 
   // ---- per-lane A rows (fixed over K): image base and the tap-independent coordinates ----
+  constexpr int AR = AI;          // A rows per lane per K-step
+  constexpr int RPW = 8;          // rows per wave-instruction (128-B rows)
   const int pc = lane & 7;        // physical 16-B chunk this lane fills
-  long a_nb[AI];                  // n * H
-  int a_h0[AI], a_w0[AI], a_row[AI];
+  long a_nb[AR];                  // n * H
+  int a_h0[AR], a_w0[AR], a_row[AR];
 #pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+  for (int i = 0; i < AR; ++i) {
+    const int row = (i * 8 + wave) * RPW + (lane >> 3);
     a_row[i] = row;
     const long m = m0 + row;
     const bool ok = m < M;
@@ -118,14 +123,20 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   auto issue_a = [&](int kb, int stage) {
     const int k0 = kb * BK;
     const int tap = k0 / a.C;
-    const int c0 = k0 - tap * a.C;
+    const int c0 = T8 ? 0 : k0 - tap * a.C;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     const int dh = kh * a.dil, dw = kw * a.dil;
     char* sA = smem + stage * STAGE_BYTES;
 #pragma unroll
-    for (int i = 0; i < AI; ++i) {
+    for (int i = 0; i < AR; ++i) {
       const int lc = swz(a_row[i], pc);
       int hi = a_h0[i] + dh, wi = a_w0[i] + dw;
+      if constexpr (T8) {   // one tap per 16-B chunk: this lane's tap is kb*8 + lc
+        const int t8 = kb * 8 + lc;
+        const int kh8 = t8 / a.KW, kw8 = t8 - kh8 * a.KW;
+        hi = t8 < a.KH * a.KW ? a_h0[i] + kh8 * a.dil : -1;
+        wi = a_w0[i] + kw8 * a.dil;
+      }
       bool ok;
       if constexpr (ST == 1) {
         ok = ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
@@ -135,7 +146,7 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
         wi /= ST;
         ok &= (hi < a.H) & (wi < a.W);
       }
-      const size_t off = ((size_t)(a_nb[i] + hi) * a.W + wi) * a.ldx + c0 + lc * 8;
+      const size_t off = ((size_t)(a_nb[i] + hi) * a.W + wi) * a.ldx + c0 + (T8 ? 0 : lc * 8);
       glds16(ok ? (const void*)(X + off) : (const void*)zero, sA + (i * 8 + wave) * 1024);
     }
   };
@@ -391,14 +402,14 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   }
 }
 
-template <int BN, int WMW, int WNW, int STAGES, int ST>
+template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0>
 hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 256;
   constexpr int STAGE_BYTES = (BM + BN) * 128;
   constexpr int EPI = BM * (64 + 4) * 4 + 64 * 8 * 8 * 4;
   constexpr int LDS = STAGES * STAGE_BYTES > EPI ? STAGES * STAGE_BYTES : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST>;
+  auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST, T8>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -415,6 +426,9 @@ hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
 
 // bf16 fast path: C % 64 == 0, ld/co multiples of 8; stats tiles are 256 rows
 bool conv_nt_v2_ok(const ConvArgs& a) {
+  if (a.tap8)   // padded stem: 8-channel taps, weights [Co][ldw >= ceil(KH*KW*8/64)*64]
+    return a.st == 1 && a.C == 8 && a.ldx == 8 && a.Co <= 64 && (a.Co % 8) == 0 && (a.ldy % 8) == 0 &&
+           a.ldw >= (a.KH * a.KW * 8 + BK - 1) / BK * BK && (a.ldw % 8) == 0 && !a.r && !a.r2;
   return (a.st == 1 || a.st == 2) && (a.C % BK) == 0 && (a.ldx % 8) == 0 && (a.ldw % 8) == 0 && (a.Co % 8) == 0 &&
          (a.ldy % 8) == 0 && (!a.r || a.ldr % 8 == 0) && (!a.r2 || a.ldr2 % 8 == 0);
 }
@@ -427,6 +441,7 @@ hipError_t v2_dispatch(const ConvArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s) {
+  if (a.tap8) return v2_launch<64, 8, 1, 3, 1, 1>(a, s);
   if (a.st == 1) return v2_dispatch<1>(a, s);
   if (a.st == 2) return v2_dispatch<2>(a, s);
   return hipErrorInvalidValue;

@@ -103,6 +103,10 @@ struct seg_ctx {
   // graph
   Act img;                        // compute-dtype images
   int stem = -1;
+  // bf16 stem as 8-channel taps (tap8): padded images [N][H][W][8] and weights [64][stem_ldw]
+  bool stem8 = false;
+  bf16_t* stem_wpad = nullptr;
+  int stem_ldw = 0;
   Act z0, dz0, p0, dp0;
   uint8_t* pool_arg = nullptr;    // max-pool first-max window index per output element
   int pool_ph = 0, pool_pw = 0;
@@ -325,11 +329,12 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
   return 0;
 }
 
-int wgrad_splits(const ConvL& L) {
+int wgrad_splits(const ConvL& L, int ci = 0) {
+  if (!ci) ci = L.ci;   // 8 for the tap8 stem
   int BM = L.co_pad <= 64 ? 64 : 128;
   int BN = 128;
-  if (L.ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, L.k * L.k * L.ci, &BM, &BN);
-  long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * L.ci + BN - 1) / BN);
+  if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, L.k * L.k * ci, &BM, &BN);
+  long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * ci + BN - 1) / BN);
   long P = (long)L.N * L.Ho * L.Wo;
   // ~2 waves of 256 single-workgroup CUs, each split >= 32 K-steps of 64 pixels
   long s = std::max<long>(1, 512 / std::max<long>(tiles, 1));
@@ -373,6 +378,9 @@ int conv_forward(Step& S, int li, const Act& x) {
   a.y = L.y.p; a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co; a.ldy = L.y.ld;
   a.KH = a.KW = L.k; a.sf = L.stride; a.st = 1; a.pad_h = L.pad_h; a.pad_w = L.pad_w;
   a.dil = L.rate; a.stats = L.stats_part;
+  if (li == c->stem && c->stem8) {
+    a.C = 8; a.ldx = 8; a.tap8 = 1; a.w = c->stem_wpad; a.ldw = c->stem_ldw;
+  }
   long M = (long)x.N * L.Ho * L.Wo;
   int slot;
   if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
@@ -473,13 +481,20 @@ int conv_wgrad(Step& S, int li, const Act& x) {
   a.x = x.p; a.N = x.N; a.H = x.H; a.W = x.W; a.C = x.C; a.ldx = x.ld;
   a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co_pad;
   a.KH = a.KW = L.k; a.sf = L.stride; a.pad_h = L.pad_h; a.pad_w = L.pad_w; a.dil = L.rate;
-  a.splits = wgrad_splits(L);
+  const bool s8 = li == c->stem && c->stem8;
+  if (s8) { a.C = 8; a.ldx = 8; }
+  a.splits = wgrad_splits(L, a.C);
   a.out = c->slab;
   long P = (long)L.N * L.Ho * L.Wo;
   int slot;
   if (int r = prof_begin(c, S.s, 2, li, 2.0 * P * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
   HIPCALL(c, launch_conv_wgrad(S.dt, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
+  if (s8) {
+    HIPCALL(c, launch_splitk_reduce_pad8(c->slab, a.splits, (long)L.co_pad * L.k * L.k * 8, L.co,
+                                         L.k * L.k, L.ci, c->grads + L.w_off, S.s));
+    return 0;
+  }
   const long n = (long)L.co * L.k * L.k * L.ci;
   // slab rows are co_pad wide only in the Co dimension: rows 0..co-1 are the real ones
   // split z of the slab starts at z*co_pad*ncol; rows >= co are padding and never reduced
@@ -628,9 +643,10 @@ int build(seg_ctx* c) {
 
   // ---- activations ----
   const int H = g.height, W = g.width;
-  if (c->dt == SEG_BF16)
-    if (int r = alloc_act(c, c->img, N, H, W, 3)) return r;
-  c->img.N = N; c->img.H = H; c->img.W = W; c->img.C = 3; c->img.ld = 3;
+  c->stem8 = c->dt == SEG_BF16;
+  if (c->stem8)
+    if (int r = alloc_act(c, c->img, N, H, W, 8)) return r;
+  c->img.N = N; c->img.H = H; c->img.W = W; c->img.C = 3; c->img.ld = c->stem8 ? 8 : 3;
   ConvL& st = c->convs[c->stem];
   if (int r = alloc_conv(c, st, N, H, W)) return r;
   if (int r = alloc_act(c, c->z0, N, st.Ho, st.Wo, 64)) return r;
@@ -710,7 +726,13 @@ int build(seg_ctx* c) {
       L.wt_lp = p;
     }
     if (c->dt == SEG_BF16) L.w_lp = (bf16_t*)c->w_lp_flat + L.w_off;
-    slab = std::max(slab, (size_t)wgrad_splits(L) * L.co_pad * L.k * L.k * L.ci);
+    const int wci = (&L == &c->convs[c->stem] && c->stem8) ? 8 : L.ci;
+    slab = std::max(slab, (size_t)wgrad_splits(L, wci) * L.co_pad * L.k * L.k * wci);
+  }
+  if (c->stem8) {
+    const ConvL& st = c->convs[c->stem];
+    c->stem_ldw = (st.k * st.k * 8 + 63) / 64 * 64;
+    if (int r = dalloc(c, &c->stem_wpad, (size_t)st.co * c->stem_ldw)) return r;
   }
   c->slab_floats = slab;
   if (int r = dalloc(c, &c->slab, slab)) return r;
@@ -779,7 +801,9 @@ Act logits_slice(seg_ctx* c, int h) {
 
 int forward(Step& S, const float* images) {
   seg_ctx* c = S.c;
-  if (c->dt == SEG_BF16) {
+  if (c->stem8) {
+    HIPCALL(c, launch_cast_pad8(images, (bf16_t*)c->img.p, c->img.M(), S.s));
+  } else if (c->dt == SEG_BF16) {
     HIPCALL(c, launch_cast_f32_bf16(images, (bf16_t*)c->img.p, c->img.M() * 3, S.s));
   } else {
     c->img.p = (void*)images;
@@ -865,13 +889,21 @@ int backward(Step& S) {
   return conv_wgrad(S, c->stem, c->img);
 }
 
+int refresh_stem_pad(seg_ctx* c, hipStream_t s) {
+  if (!c->stem8) return 0;
+  const ConvL& st = c->convs[c->stem];
+  HIPCALL(c, launch_stem_pad_weights((const bf16_t*)st.w_lp, c->stem_wpad, st.co, st.k * st.k, st.ci,
+                                     c->stem_ldw, s));
+  return 0;
+}
+
 int refresh_compute_weights(seg_ctx* c, hipStream_t s) {
   if (c->dt == SEG_BF16)
     HIPCALL(c, launch_cast_f32_bf16(c->params, (bf16_t*)c->w_lp_flat, c->n_decay, s));
   for (auto& L : c->convs)
     if (L.wt_lp)
       HIPCALL(c, launch_weight_flip_transpose(c->dt, L.w_lp, L.wt_lp, L.co, L.k, L.k, L.ci, s));
-  return 0;
+  return refresh_stem_pad(c, s);
 }
 
 }  // namespace
@@ -1024,7 +1056,7 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
   for (auto& L : c->convs)
     if (L.wt_lp)
       HIPCALL(c, launch_weight_flip_transpose(c->dt, L.w_lp, L.wt_lp, L.co, L.k, L.k, L.ci, s));
-  return 0;
+  return refresh_stem_pad(c, s);
 }
 
 int seg_outputs(seg_ctx* c, const float** losses, const float** reg, const float** logits,

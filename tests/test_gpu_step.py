@@ -268,4 +268,10 @@ def test_bf16_backward_layerwise(cuda):
             assert _rel(grads[sp.name + "/weights"], ref) < 2e-2, (sp.name, _rel(grads[sp.name + "/weights"], ref))
         checked += 1
     assert checked == 16 + 3   # R50 units + adaptation bottlenecks
+    # the 7x7/2 stem (bf16: 3 channels padded to 8-channel taps) weight gradient
+    sp = specs[0]
+    w = wbf(sp.name).requires_grad_(True)
+    conv_tf(T(ctx.debug_tensor("conv0_x")), w, sp).backward(T(ctx.debug_tensor("conv0_dy")))
+    ref = w.grad.numpy().reshape(-1)
+    assert _rel(grads[sp.name + "/weights"], ref) < 2e-2, _rel(grads[sp.name + "/weights"], ref)
     ctx.close()
