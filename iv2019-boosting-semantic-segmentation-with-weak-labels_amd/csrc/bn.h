@@ -28,11 +28,13 @@ struct BnApplyArgs {
   // residual 2: second BN (shortcut conv): (y2-mean2)*scale2+beta2
   const void* y2; int ldy2; const float* mean2; const float* scale2; const float* beta2;
   void* out; int ldo;              // output (T or f32)
+  uint8_t* mask;                   // optional ReLU bits of out: [M][C/8], bit e = out[c0+e] > 0
 };
 
 struct BnBwdArgs {
   const void* dz; int lddz;        // incoming gradient (T or f32)
   const void* z; int ldz;          // activation whose >0 mask gates dz (nullable)
+  const uint8_t* mask;             // the same gate as bits [M][C/8] (preferred over z when set)
   const void* y; int ldy;          // conv output (T)
   long M; int C;
   const float* mean; const float* invstd; const float* scale;

@@ -342,12 +342,21 @@ __global__ __launch_bounds__(256) void bn_apply8_kernel(BnApplyArgs a) {
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float x = __builtin_fmaf(v[k][e] - mu[e], sc[e], be[e]);   // = conv_v2 fused mask
+        float x = __builtin_fmaf(v[k][e] - mu[e], sc[e], be[e]);
         if constexpr (RES == RES_BN2) x = __builtin_fmaf(u[k][e] - mu2[e], sc2[e], be2[e]) + x;
         else if constexpr (RES != RES_NONE) x = u[k][e] + x;
         o[e] = RELU ? fmaxf(x, 0.f) : x;
       }
       Vec8<TO>::store(O + (size_t)(base + k * L.rpp) * a.ldo, o);
+      if (RELU && a.mask) {   // bits of the value as stored (> 0 after rounding)
+        uint32_t bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool pos = sizeof(TO) == 2 ? f2bf(o[e]) != 0 : o[e] > 0.f;
+          bits |= (uint32_t)pos << e;
+        }
+        a.mask[(size_t)(base + k * L.rpp) * (a.C >> 3) + L.cg] = (uint8_t)bits;
+      }
     }
   };
   long base = (long)blockIdx.x * step + L.rl;
@@ -385,13 +394,16 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
   const T* Y = (const T*)a.y + c0;
   Raw8<TZ> rdz[BN_U], rz[BN_U];
   Raw8<T> ry[BN_U];
+  uint32_t mk[BN_U];
+  const int cg = c0 >> 3, cgn = a.C >> 3;
 #pragma unroll
   for (int k = 0; k < BN_U; ++k) {
     if (FULL || k < nrows) {
       const size_t m = (size_t)(base + k * rpp);
       rdz[k].load(DZ + m * a.lddz);
       ry[k].load(Y + m * a.ldy);
-      if constexpr (HZ) rz[k].load(Z + m * a.ldz);
+      if constexpr (HZ == 1) rz[k].load(Z + m * a.ldz);
+      if constexpr (HZ == 2) mk[k] = a.mask[m * cgn + cg];
     }
   }
   __builtin_amdgcn_sched_barrier(0);   // keep the group's loads ahead of every conversion
@@ -400,11 +412,14 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
     if (FULL || k < nrows) {
       rdz[k].cvt(dz[k]);
       ry[k].cvt(y[k]);
-      if constexpr (HZ) {
+      if constexpr (HZ == 1) {
         float z[8];
         rz[k].cvt(z);
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[k][e] = z[e] > 0.f ? dz[k][e] : 0.f;
+      } else if constexpr (HZ == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[k][e] = (mk[k] >> e) & 1u ? dz[k][e] : 0.f;
       }
     } else {
 #pragma unroll
@@ -565,10 +580,12 @@ bool bwd_v8(const BnBwdArgs& a) {
 
 template <typename T, typename TZ>
 hipError_t bwd_reduce_t(const BnBwdArgs& a, hipStream_t s) {
+  if (a.mask && !bwd_v8<T, TZ>(a)) return hipErrorInvalidValue;   // bits exist on the 8-wide path only
   if (bwd_v8<T, TZ>(a)) {
     const int cg_n = a.C / 8;
     const dim3 g(a.rb, cg_n > 256 ? ceil_div(cg_n, 256) : 1);
-    if (a.z && a.dzscale) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 1, 1>), g, dim3(256), 0, s, a);
+    if (a.mask) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 0>), g, dim3(256), 0, s, a);
+    else if (a.z && a.dzscale) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 1, 1>), g, dim3(256), 0, s, a);
     else if (a.z) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 1, 0>), g, dim3(256), 0, s, a);
     else if (a.dzscale) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 0, 1>), g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 0, 0>), g, dim3(256), 0, s, a);
@@ -579,9 +596,15 @@ hipError_t bwd_reduce_t(const BnBwdArgs& a, hipStream_t s) {
 
 template <typename T, typename TZ>
 hipError_t bwd_apply_t(const BnBwdArgs& a, hipStream_t s) {
+  if (a.mask && !bwd_v8<T, TZ>(a)) return hipErrorInvalidValue;
   if (bwd_v8<T, TZ>(a)) {
     const dim3 g = grid8(a.M, a.C);
     const int key = (a.z ? 4 : 0) | (a.dzscale ? 2 : 0) | (a.dyhat ? 1 : 0);
+    if (a.mask) {   // ReLU bits (never combined with dzscale: that is the logits BN, no ReLU)
+      if (a.dyhat) hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 0, 1>), g, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 0, 0>), g, dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
     switch (key) {
       case 0: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 0, 0, 0>), g, dim3(256), 0, s, a); break;
       case 1: hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 0, 0, 1>), g, dim3(256), 0, s, a); break;

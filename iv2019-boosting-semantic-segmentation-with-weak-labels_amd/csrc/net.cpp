@@ -37,6 +37,7 @@ int set_err(std::string* dst, int code, const char* fmt, ...) {
 struct Act {
   void* p = nullptr;
   int N = 0, H = 0, W = 0, C = 0, ld = 0;
+  uint8_t* mask = nullptr;   // ReLU bits [M][C/8] of a BN+ReLU output (read by the backward)
   long M() const { return (long)N * H * W; }
 };
 
@@ -175,6 +176,13 @@ int alloc_act(seg_ctx* c, Act& a, int N, int H, int W, int C, int ld = 0, size_t
   int r = dalloc(c, &p, (size_t)a.M() * a.ld * e);
   a.p = p;
   return r;
+}
+
+// ReLU-output activation with its bit mask (C % 8 == 0)
+int alloc_relu_act(seg_ctx* c, Act& a, int N, int H, int W, int C, int ld = 0) {
+  if (int r = alloc_act(c, a, N, H, W, C, ld)) return r;
+  if (C % 8) return 0;
+  return dalloc(c, &a.mask, (size_t)a.M() * (C / 8));
 }
 
 Act slice(const seg_ctx* c, const Act& a, int c_off, int C) {
@@ -410,6 +418,7 @@ int bn_apply(Step& S, int li, const Act& out, int out_f32, const Act* res = null
     a.beta2 = c->params + L2.b_off;
   }
   a.out = out.p; a.ldo = out.ld;
+  a.mask = a.relu ? out.mask : nullptr;
   const double esz = S.dt == SEG_BF16 ? 2.0 : 4.0;
   const double gb = a.M * (double)a.C * (esz * (1 + (a.res || a.y2 ? 1 : 0)) +
                                          (out_f32 ? 4.0 : esz)) * 1e-9;
@@ -427,6 +436,7 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   BnBwdArgs a{};
   a.dz = dz.p; a.lddz = dz.ld;
   if (z) { a.z = z->p; a.ldz = z->ld; }
+  if (z && z->mask && !dz_f32 && !dzscale && z->C == L.co) { a.mask = z->mask; a.z = nullptr; }
   a.y = L.y.p; a.ldy = L.y.ld; a.M = L.y.M(); a.C = L.co;
   a.mean = L.st.mean; a.invstd = L.st.invstd; a.scale = L.st.scale;
   a.sdy = L.st.sdy; a.sdyx = L.st.sdyx;
@@ -436,7 +446,7 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   a.dzscale = dzscale;
   const double esz = S.dt == SEG_BF16 ? 2.0 : 4.0, zsz = dz_f32 ? 4.0 : esz;
   const double me = a.M * (double)a.C * 1e-9;
-  const double gb_in = me * (zsz * (z ? 2 : 1) + esz);
+  const double gb_in = me * (zsz + (a.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
   int slot;
   if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
   HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
@@ -573,15 +583,15 @@ int alloc_unit(seg_ctx* c, Unit& u, const Act& in) {
     if (int r = alloc_conv(c, c->convs[u.sc], in.N, in.H, in.W)) return r;
   ConvL& c1 = c->convs[u.c1];
   if (int r = alloc_conv(c, c1, in.N, in.H, in.W)) return r;
-  if (int r = alloc_act(c, u.z1, in.N, c1.Ho, c1.Wo, c1.co)) return r;
+  if (int r = alloc_relu_act(c, u.z1, in.N, c1.Ho, c1.Wo, c1.co)) return r;
   if (int r = alloc_act(c, u.dz1, in.N, c1.Ho, c1.Wo, c1.co)) return r;
   ConvL& c2 = c->convs[u.c2];
   if (int r = alloc_conv(c, c2, in.N, c1.Ho, c1.Wo)) return r;
-  if (int r = alloc_act(c, u.z2, in.N, c2.Ho, c2.Wo, c2.co)) return r;
+  if (int r = alloc_relu_act(c, u.z2, in.N, c2.Ho, c2.Wo, c2.co)) return r;
   if (int r = alloc_act(c, u.dz2, in.N, c2.Ho, c2.Wo, c2.co)) return r;
   ConvL& c3 = c->convs[u.c3];
   if (int r = alloc_conv(c, c3, in.N, c2.Ho, c2.Wo)) return r;
-  if (int r = alloc_act(c, u.out, in.N, c3.Ho, c3.Wo, c3.co)) return r;
+  if (int r = alloc_relu_act(c, u.out, in.N, c3.Ho, c3.Wo, c3.co)) return r;
   if (int r = alloc_act(c, u.dout, in.N, c3.Ho, c3.Wo, c3.co)) return r;
   if (u.kind != SC_CONV)
     if (int r = alloc_act(c, u.dpre, in.N, c3.Ho, c3.Wo, c3.co)) return r;
@@ -649,7 +659,7 @@ int build(seg_ctx* c) {
   c->img.N = N; c->img.H = H; c->img.W = W; c->img.C = 3; c->img.ld = c->stem8 ? 8 : 3;
   ConvL& st = c->convs[c->stem];
   if (int r = alloc_conv(c, st, N, H, W)) return r;
-  if (int r = alloc_act(c, c->z0, N, st.Ho, st.Wo, 64)) return r;
+  if (int r = alloc_relu_act(c, c->z0, N, st.Ho, st.Wo, 64)) return r;
   if (int r = alloc_act(c, c->dz0, N, st.Ho, st.Wo, 64)) return r;
   {  // max_pool2d 3x3/2 SAME
     int Ho = (st.Ho + 1) / 2, Wo = (st.Wo + 1) / 2;
@@ -694,10 +704,10 @@ int build(seg_ctx* c) {
     }
     if (int r = dalloc(c, &c->grid_part, gp)) return r;
     if (int r = alloc_conv(c, c->convs[c->pyr_final], N, Hf, Wf)) return r;
-    if (int r = alloc_act(c, c->feat, N, Hf, Wf, fd)) return r;
+    if (int r = alloc_relu_act(c, c->feat, N, Hf, Wf, fd)) return r;
     if (int r = alloc_act(c, c->dfeat, N, Hf, Wf, fd)) return r;
   } else {
-    if (int r = alloc_act(c, c->z_dfd, N, Hf, Wf, fd)) return r;
+    if (int r = alloc_relu_act(c, c->z_dfd, N, Hf, Wf, fd)) return r;
     c->feat = c->z_dfd;
     c->dfeat = c->dz_dfd;
   }
