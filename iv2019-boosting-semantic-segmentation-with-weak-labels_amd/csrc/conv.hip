@@ -513,7 +513,16 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, int splits,
   long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i4 + 3 < n && (stride & 3) == 0) {
     float4 s = accumulate ? *(const float4*)(out + i4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int z = 0; z < splits; ++z) {
+    // loads of 8 slabs in flight, summed in slab order (same result as the serial loop)
+    int z = 0;
+    for (; z + 8 <= splits; z += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = *(const float4*)(part + (size_t)(z + k) * stride + i4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
+    }
+    for (; z < splits; ++z) {
       float4 v = *(const float4*)(part + (size_t)z * stride + i4);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }

@@ -155,6 +155,66 @@ __global__ void grid_rowreduce_kernel(const T* __restrict__ x, int N, int H, int
   }
 }
 
+// 8 channels per thread (16-B loads), RL row lanes stride the row's pixels, cells taken 6 at a
+// time (a second sweep of the row for 7..12 cells keeps the accumulators in registers); per-cell
+// partial sums combined over the row lanes through LDS in fixed order.
+// C % 8 == 0, 256 % (C/8) == 0, total cells <= 12.
+template <typename T>
+__global__ __launch_bounds__(256) void grid_rowreduce8_kernel(const T* __restrict__ x, int N, int H, int W,
+                                                              int C, int ldx, GridSpec g,
+                                                              float* __restrict__ part) {
+  constexpr int QB = 6;
+  const int n = blockIdx.x / H, h = blockIdx.x % H;
+  const int cgn = C >> 3, RL = 256 / cgn;
+  const int cg = threadIdx.x % cgn, rl = threadIdx.x / cgn;
+  __shared__ float tab[QB * 256];
+  __shared__ float red[256 * 8];
+  const T* row = x + (size_t)((long)n * H + h) * W * ldx + cg * 8;
+  float* o = part + (size_t)((long)n * H + h) * g.total_ccells * C;
+  for (int q0 = 0; q0 < g.total_ccells; q0 += QB) {
+    const int nq = g.total_ccells - q0 < QB ? g.total_ccells - q0 : QB;
+    float acc[QB][8];
+#pragma unroll
+    for (int q = 0; q < QB; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[q][e] = 0.f;
+    for (int w0 = 0; w0 < W; w0 += 256) {
+      const int wn = (W - w0) < 256 ? (W - w0) : 256;
+      __syncthreads();
+      for (int i = threadIdx.x; i < nq * wn; i += 256) {
+        const int q = i / wn, w = i - q * wn;
+        tab[q * 256 + w] = g.rowtab[(size_t)(q0 + q) * W + w0 + w];
+      }
+      __syncthreads();
+      for (int w = rl; w < wn; w += RL) {
+        float v[8];
+        Vec8<T>::load(row + (size_t)(w0 + w) * ldx, v);
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+          if (q < nq) {
+            const float wq = tab[q * 256 + w];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[q][e] = __builtin_fmaf(wq, v[e], acc[q][e]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      if (q >= nq) break;
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[(rl * cgn + cg) * 8 + e] = acc[q][e];
+      __syncthreads();
+      for (int c = threadIdx.x; c < C; c += 256) {
+        float t = 0.f;
+        for (int r = 0; r < RL; ++r) t += red[r * C + c];
+        o[(size_t)(q0 + q) * C + c] = t;
+      }
+    }
+  }
+}
+
 struct OutPtrs { void* p[SEG_MAX_GRIDS]; };
 
 template <typename T>
@@ -305,6 +365,14 @@ hipError_t launch_grid_rowreduce(int dtype, const void* x, int N, int H, int W, 
                                  const GridSpec& g, float* part, hipStream_t s) {
   if (g.total_ccells > SEG_MAX_CELLS) return hipErrorInvalidValue;
   dim3 gr(N * H);
+  const bool v8 = C % 8 == 0 && ldx % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0 && g.total_ccells <= 12;
+  if (v8) {
+    if (dtype == SEG_BF16)
+      hipLaunchKernelGGL((grid_rowreduce8_kernel<bf16_t>), gr, dim3(256), 0, s, (const bf16_t*)x, N, H, W, C, ldx, g, part);
+    else
+      hipLaunchKernelGGL((grid_rowreduce8_kernel<float>), gr, dim3(256), 0, s, (const float*)x, N, H, W, C, ldx, g, part);
+    return hipGetLastError();
+  }
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(grid_rowreduce_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)x, N, H,
                        W, C, ldx, g, part);
