@@ -59,12 +59,20 @@ template <> struct OutT<1> { typedef float T; };
 // (Measured and rejected: splitting each stage into two 32-deep units refilled one phase
 // after their last read -- 1.5 K-steps of prefetch instead of 1 -- ran 5-8 % slower: the
 // extra barrier per K-step costs more than the deeper prefetch gains.)
-template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0>
+template <int MF> struct AccOf;
+template <> struct AccOf<16> { typedef f32x4_t T; static constexpr int N = 4; };
+
+// MF: MFMA shape (16: v_mfma_f32_16x16x32_bf16). A v_mfma_f32_32x32x16_bf16 main loop with
+// fragments double-buffered across k16-steps was measured 5-9 % slower on the C2 layer shapes
+// and removed; the epilogue keeps the shape-generic (row_of / col_of) accumulator walk.
+template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16>
 __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   const bf16_t* zero = g_zero16;
   constexpr int BM = 256;
   constexpr int WM = BM / WMW, WN = BN / WNW;
-  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int FM = WM / MF, FN = WN / MF;
+  constexpr int NA = AccOf<MF>::N;   // accumulator elements per lane per fragment
+  typedef typename AccOf<MF>::T acc_t;
   constexpr int AI = BM * 8 / V2_THREADS;       // A glds per lane per K-step (4)
   constexpr int BI = BN * 8 / V2_THREADS;       // B glds per lane per K-step
   constexpr int LPK = AI + BI;
@@ -163,11 +171,23 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
     }
   };
 
-  f32x4_t acc[FM][FN];
+  acc_t acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int k = 0; k < NA; ++k) acc[i][j][k] = 0.f;
+  // accumulator element (i, j, k) -> tile row / column
+  auto row_of = [&](int i, int k) {
+    if constexpr (MF == 16) return wm * WM + i * 16 + lq * 4 + k;
+    else return wm * WM + i * 32 + (k >> 2) * 8 + (lane >> 5) * 4 + (k & 3);
+  };
+  auto col_of = [&](int j) {
+    if constexpr (MF == 16) return wn * WN + j * 16 + lr;
+    else return wn * WN + j * 32 + (lane & 31);
+  };
+  const bool col_writer = MF == 16 ? lq == 0 : lane < 32;   // one lane per column after merges
 
   // one K-step of MFMAs; the next stage's LDS-DMA is issued in two parts, one ahead of each
   // 32-deep k-substep, so its issue cost spreads over the MFMA stream
@@ -232,7 +252,7 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
     // rows from (sum, sum of squares); then Chan merges of equal-count groups over the lane
     // groups (shfl 16, 32) and the WMW waves (LDS), fixed order
     float2* red2 = (float2*)smem;     // [WMW][BN] (sum, M2)
-    constexpr float NL = 4.f * FM;    // rows per lane
+    constexpr float NL = (float)(NA * FM);   // rows per lane
     float sj[FN], mj[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -240,8 +260,8 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float x = acc[i][j][r];
+        for (int k = 0; k < NA; ++k) {
+          const float x = acc[i][j][k];
           sm += x;
           sq = __builtin_fmaf(x, x, sq);
         }
@@ -250,7 +270,7 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
     }
     float n = NL;
 #pragma unroll
-    for (int o = 16; o <= 32; o <<= 1) {
+    for (int o = MF; o <= 32; o <<= 1) {   // lanes holding other rows of the same column
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
@@ -260,14 +280,14 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
       }
       n *= 2.f;
     }
-    if (lq == 0)
+    if (col_writer)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) red2[wm * BN + wn * WN + j * 16 + lr] = make_float2(sj[j], mj[j]);
+      for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
     __syncthreads();
-    if (wm == 0 && lq == 0) {
+    if (wm == 0 && col_writer) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int c = wn * WN + j * 16 + lr;
+        const int c = col_of(j);
         float2 t = red2[c];
         float nt = (float)WM;
 #pragma unroll
@@ -293,23 +313,19 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * WM + i * 16 + lq * 4 + r;
-          const float x = row < rows_valid ? acc[i][j][r] : 0.f;
-          v += x;
-        }
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
+        for (int k = 0; k < NA; ++k) v += row_of(i, k) < rows_valid ? acc[i][j][k] : 0.f;
+#pragma unroll
+      for (int o = MF; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
       cs[j] = v;
     }
-    if (lq == 0)
+    if (col_writer)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + wn * WN + j * 16 + lr] = cs[j];
+      for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
     __syncthreads();
     float mean[FN], tot[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int c = wn * WN + j * 16 + lr;
+      const int c = col_of(j);
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
@@ -322,24 +338,23 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * WM + i * 16 + lq * 4 + r;
-          const float d = acc[i][j][r] - mean[j];
-          v += row < rows_valid ? d * d : 0.f;
+        for (int k = 0; k < NA; ++k) {
+          const float d = acc[i][j][k] - mean[j];
+          v += row_of(i, k) < rows_valid ? d * d : 0.f;
         }
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
+#pragma unroll
+      for (int o = MF; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
       cs[j] = v;
     }
     __syncthreads();
-    if (lq == 0)
+    if (col_writer)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + wn * WN + j * 16 + lr] = cs[j];
+      for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
     __syncthreads();
-    if (wm == 0 && lq == 0) {
+    if (wm == 0 && col_writer) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int c = wn * WN + j * 16 + lr;
+        const int c = col_of(j);
         float t = 0.f;
 #pragma unroll
         for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
@@ -361,13 +376,12 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
     if (wn * WN + WN > cbase && wn * WN < cbase + EPI_COLS) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int col = wn * WN + j * 16 + lr;
+        const int col = col_of(j);
         if (col >= cbase && col < cbase + EPI_COLS) {
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              stage[(wm * WM + i * 16 + lq * 4 + r) * EPI_LD + (col - cbase)] = acc[i][j][r];
+            for (int k = 0; k < NA; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = acc[i][j][k];
         }
       }
     }
@@ -402,14 +416,14 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   }
 }
 
-template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0>
+template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16>
 hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 256;
   constexpr int STAGE_BYTES = (BM + BN) * 128;
   constexpr int EPI = BM * (64 + 4) * 4 + 64 * 8 * 8 * 4;
   constexpr int LDS = STAGES * STAGE_BYTES > EPI ? STAGES * STAGE_BYTES : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST, T8>;
+  auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST, T8, MF>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
