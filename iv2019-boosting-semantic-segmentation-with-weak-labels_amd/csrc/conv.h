@@ -46,6 +46,10 @@ hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t
 hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s);
 hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride, long n,
                                 float* out, int accumulate, hipStream_t s);
+// all layers' flips in one launch: table of FlipJob (device), prefix = first output element
+struct FlipJob { const void* w; void* wt; int co, k, ci; long prefix; };
+hipError_t launch_weight_flip_batched(int dtype, const FlipJob* jobs, int njobs, long total,
+                                      hipStream_t s);
 hipError_t launch_weight_flip_transpose(int dtype, const void* w, void* wt, int co, int kh, int kw,
                                         int ci, hipStream_t s);
 int conv_nt_mtiles(long M);  // upper bound on BN-stat partial tiles (128-row tiles)

@@ -552,6 +552,26 @@ __global__ void weight_flip_transpose_kernel(const T* __restrict__ w, T* __restr
   wt[i] = w[(((size_t)o * kh + (kh - 1 - y)) * kw + (kw - 1 - x)) * ci + c];
 }
 
+template <typename T>
+__global__ void weight_flip_batched_kernel(const FlipJob* __restrict__ jobs, int njobs, long total) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = njobs - 1;   // last job with prefix <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].prefix <= i) lo = mid; else hi = mid - 1;
+    }
+    const FlipJob J = jobs[lo];
+    const long r = i - J.prefix;   // index over [ci][k][k][co]
+    const int o = (int)(r % J.co);
+    long t = r / J.co;
+    const int x = (int)(t % J.k);
+    t /= J.k;
+    const int y = (int)(t % J.k);
+    const int c = (int)(t / J.k);
+    ((T*)J.wt)[r] = ((const T*)J.w)[(((size_t)o * J.k + (J.k - 1 - y)) * J.k + (J.k - 1 - x)) * J.ci + c];
+  }
+}
+
 template <typename T, typename TO, int BM, int BN, bool G>
 hipError_t nt_launch(const ConvArgs& a, hipStream_t s) {
   long M = (long)a.N * a.Ho * a.Wo;
@@ -673,6 +693,17 @@ hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride
   long threads = (n + 3) / 4;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, s, part,
                      splits, split_stride, n, out, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_weight_flip_batched(int dtype, const FlipJob* jobs, int njobs, long total,
+                                      hipStream_t s) {
+  long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(weight_flip_batched_kernel<bf16_t>, dim3((int)g), dim3(256), 0, s, jobs, njobs, total);
+  else
+    hipLaunchKernelGGL(weight_flip_batched_kernel<float>, dim3((int)g), dim3(256), 0, s, jobs, njobs, total);
   return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@ namespace {
 constexpr int LA = 4;     // owned low-res rows per block
 constexpr int LB = 30;    // owned low-res cols per block
 constexpr int THREADS = 256;
+constexpr int GLD = THREADS + 1;   // gbuf row stride
 
 __device__ __forceinline__ void lerp_of(int o, int n_in, int n_out, int& lo, int& hi, float& l) {
   // TF ResizeBilinear legacy scaler, align_corners=True
@@ -48,9 +49,12 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
   constexpr int PAIRS = LB * CT;
   constexpr int PPT = (PAIRS + THREADS - 1) / THREADS;  // owned (col, ch) pairs per thread
   __shared__ float win[WIN_R * WIN_C * CT];
-  __shared__ float gbuf[CT * THREADS];
+  __shared__ float gbuf[CT * GLD];   // [channel][pixel], padded: (c, w) -> bank (c + w) % 64
   __shared__ int wstart[LB + 3];
   __shared__ int rng[4];
+  constexpr int XT = 512;          // per-block x-lerp table (full-res columns of the footprint)
+  __shared__ float xlt[XT];        // xl(w)
+  __shared__ short xlo_t[XT], xhi_t[XT];
   __shared__ float red[6][THREADS / 64];
 
   const int tid = threadIdx.x;
@@ -80,6 +84,18 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
   }
   __syncthreads();
   const int h_begin = rng[0], h_end = rng[1], w_begin = rng[2], w_end = rng[3];
+  const bool use_xt = w_end - w_begin <= XT;
+  if (use_xt) {
+    for (int w = w_begin + tid; w < w_end; w += THREADS) {
+      int lo, hi;
+      float xl;
+      lerp_of(w, a.Wl, a.W, lo, hi, xl);
+      xlt[w - w_begin] = xl;
+      xlo_t[w - w_begin] = (short)lo;
+      xhi_t[w - w_begin] = (short)hi;
+    }
+    __syncthreads();
+  }
 
   float acc[PPT][LA];
 #pragma unroll
@@ -109,7 +125,8 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
       if (w < w_end) {
         int xlo, xhi;
         float xl;
-        lerp_of(w, a.Wl, a.W, xlo, xhi, xl);
+        if (use_xt) { xl = xlt[w - w_begin]; xlo = xlo_t[w - w_begin]; xhi = xhi_t[w - w_begin]; }
+        else lerp_of(w, a.Wl, a.W, xlo, xhi, xl);
         const float* tl = win + (((ylo - (i0 - 1)) * WIN_C) + (xlo - (j0 - 1))) * CT;
         const float* tr = win + (((ylo - (i0 - 1)) * WIN_C) + (xhi - (j0 - 1))) * CT;
         const float* bl = win + (((yhi - (i0 - 1)) * WIN_C) + (xlo - (j0 - 1))) * CT;
@@ -130,9 +147,10 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
           for (int c = 1; c < C1; ++c) m1 = fmaxf(m1, x[c]);
           float s = 0.f;
 #pragma unroll
-          for (int c = 0; c < C1; ++c) { p[c] = expf(x[c] - m1); s += p[c]; }
+          for (int c = 0; c < C1; ++c) { p[c] = __expf(x[c] - m1); s += p[c]; }
+          const float rs = 1.f / s;
 #pragma unroll
-          for (int c = 0; c < C1; ++c) p[c] = p[c] / s;
+          for (int c = 0; c < C1; ++c) p[c] = p[c] * rs;
           lse1 = logf(s);
         }
         {
@@ -141,9 +159,10 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
           for (int c = 1; c < C2; ++c) m2 = fmaxf(m2, x[C1 + c]);
           float s = 0.f;
 #pragma unroll
-          for (int c = 0; c < C2; ++c) { p[C1 + c] = expf(x[C1 + c] - m2); s += p[C1 + c]; }
+          for (int c = 0; c < C2; ++c) { p[C1 + c] = __expf(x[C1 + c] - m2); s += p[C1 + c]; }
+          const float rs = 1.f / s;
 #pragma unroll
-          for (int c = 0; c < C2; ++c) p[C1 + c] = p[C1 + c] / s;
+          for (int c = 0; c < C2; ++c) p[C1 + c] = p[C1 + c] * rs;
           lse2 = logf(s);
         }
         {
@@ -152,9 +171,10 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
           for (int c = 1; c < C3; ++c) m3 = fmaxf(m3, x[C1 + C2 + c]);
           float s = 0.f;
 #pragma unroll
-          for (int c = 0; c < C3; ++c) { p[C1 + C2 + c] = expf(x[C1 + C2 + c] - m3); s += p[C1 + C2 + c]; }
+          for (int c = 0; c < C3; ++c) { p[C1 + C2 + c] = __expf(x[C1 + C2 + c] - m3); s += p[C1 + C2 + c]; }
+          const float rs = 1.f / s;
 #pragma unroll
-          for (int c = 0; c < C3; ++c) p[C1 + C2 + c] = p[C1 + C2 + c] / s;
+          for (int c = 0; c < C3; ++c) p[C1 + C2 + c] = p[C1 + C2 + c] * rs;
           lse3 = logf(s);
         }
         // l1 argmax over probabilities (first max)
@@ -249,11 +269,11 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
         // ---- gradients: TF xent backprop = p - y, times the weight ----
 #pragma unroll
         for (int c = 0; c < C1; ++c)
-          gbuf[c * THREADS + tid] = strong ? w1 * (p[c] - (c == l1lab ? 1.f : 0.f)) : 0.f;
+          gbuf[c * GLD + tid] = strong ? w1 * (p[c] - (c == l1lab ? 1.f : 0.f)) : 0.f;
 #pragma unroll
-        for (int c = 0; c < C2; ++c) gbuf[(C1 + c) * THREADS + tid] = w2 * (p[C1 + c] - y2[c]);
+        for (int c = 0; c < C2; ++c) gbuf[(C1 + c) * GLD + tid] = w2 * (p[C1 + c] - y2[c]);
 #pragma unroll
-        for (int c = 0; c < C3; ++c) gbuf[(C1 + C2 + c) * THREADS + tid] = w3 * (p[C1 + C2 + c] - y3[c]);
+        for (int c = 0; c < C3; ++c) gbuf[(C1 + C2 + c) * GLD + tid] = w3 * (p[C1 + C2 + c] - y3[c]);
       }
       __syncthreads();
       // ---- x-reduction into owned columns: rowacc(j) ----
@@ -271,8 +291,9 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
             for (int w = wa; w < wb; ++w) {
               int lo, hi;
               float xl;
-              lerp_of(w, a.Wl, a.W, lo, hi, xl);
-              float gv = gbuf[c * THREADS + (w - wc)];
+              if (use_xt) { xl = xlt[w - w_begin]; lo = xlo_t[w - w_begin]; hi = xhi_t[w - w_begin]; }
+              else lerp_of(w, a.Wl, a.W, lo, hi, xl);
+              float gv = gbuf[c * GLD + (w - wc)];
               sacc += gv * (1.f - xl);
               if (hi == lo) sacc += gv * xl;
             }
@@ -282,8 +303,9 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
             for (int w = wa; w < wb; ++w) {
               int lo, hi;
               float xl;
-              lerp_of(w, a.Wl, a.W, lo, hi, xl);
-              if (hi == j) sacc += gbuf[c * THREADS + (w - wc)] * xl;
+              if (use_xt) { xl = xlt[w - w_begin]; lo = xlo_t[w - w_begin]; hi = xhi_t[w - w_begin]; }
+              else lerp_of(w, a.Wl, a.W, lo, hi, xl);
+              if (hi == j) sacc += gbuf[c * GLD + (w - wc)] * xl;
             }
             rowacc[u] += sacc;
           }

@@ -106,6 +106,9 @@ struct seg_ctx {
   int stem = -1;
   // bf16 stem as 8-channel taps (tap8): padded images [N][H][W][8] and weights [64][stem_ldw]
   bool stem8 = false;
+  FlipJob* flip_jobs = nullptr;   // device table: every dgrad weight flip in one launch
+  int n_flip = 0;
+  long flip_total = 0;
   bf16_t* stem_wpad = nullptr;
   int stem_ldw = 0;
   Act z0, dz0, p0, dp0;
@@ -910,9 +913,7 @@ int refresh_stem_pad(seg_ctx* c, hipStream_t s) {
 int refresh_compute_weights(seg_ctx* c, hipStream_t s) {
   if (c->dt == SEG_BF16)
     HIPCALL(c, launch_cast_f32_bf16(c->params, (bf16_t*)c->w_lp_flat, c->n_decay, s));
-  for (auto& L : c->convs)
-    if (L.wt_lp)
-      HIPCALL(c, launch_weight_flip_transpose(c->dt, L.w_lp, L.wt_lp, L.co, L.k, L.k, L.ci, s));
+  if (c->n_flip) HIPCALL(c, launch_weight_flip_batched(c->dt, c->flip_jobs, c->n_flip, c->flip_total, s));
   return refresh_stem_pad(c, s);
 }
 
@@ -974,6 +975,21 @@ int seg_bind_buffers(seg_ctx* c, float* params, float* grads, float* momentum, f
     // batch statistics land directly in the gradient tail (one all-reduce covers them)
     L.st.mean = grads + c->n_train + L.mv_off;
     L.st.var_unb = grads + c->n_train + half + L.mv_off;
+  }
+  // the batched flip table needs the compute-weight pointers (fp32: the bound params)
+  std::vector<FlipJob> jobs;
+  long tot = 0;
+  for (auto& L : c->convs)
+    if (L.wt_lp) {
+      jobs.push_back({L.w_lp, L.wt_lp, L.co, L.k, L.ci, tot});
+      tot += (long)L.co * L.k * L.k * L.ci;
+    }
+  c->n_flip = (int)jobs.size();
+  c->flip_total = tot;
+  if (c->n_flip) {
+    if (!c->flip_jobs)
+      if (int r = dalloc(c, &c->flip_jobs, jobs.size())) return r;
+    HIPCALL(c, hipMemcpy(c->flip_jobs, jobs.data(), jobs.size() * sizeof(FlipJob), hipMemcpyHostToDevice));
   }
   c->bound = true;
   return 0;
@@ -1063,9 +1079,7 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
   const long half = c->n_moving / 2;
   HIPCALL(c, launch_moving_update(c->moving, c->moving + half, c->grads + c->n_train,
                                   c->grads + c->n_train + half, (int)half, c->cfg.bn_decay, s));
-  for (auto& L : c->convs)
-    if (L.wt_lp)
-      HIPCALL(c, launch_weight_flip_transpose(c->dt, L.w_lp, L.wt_lp, L.co, L.k, L.k, L.ci, s));
+  if (c->n_flip) HIPCALL(c, launch_weight_flip_batched(c->dt, c->flip_jobs, c->n_flip, c->flip_total, s));
   return refresh_stem_pad(c, s);
 }
 
