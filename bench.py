@@ -5,8 +5,9 @@
           --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
 
 Workload (BASELINE config C2, the metric's single-GPU configuration): ResNet-50 dilated
-(output stride 8) + PSP pyramid (the reference's live pyramid; ASPP exists only as a
-comment in the reference), 1024x2048 crops, 4 per-pixel-labelled images per GPU, bf16
+(output stride 8) + ASPP (as C2 names it; the reference's commented-out _create_aspp_module,
+hierarchical.py:209-226 -- `--pyramid psp` runs the reference's live PSP module instead),
+1024x2048 crops, 4 per-pixel-labelled images per GPU, bf16
 storage with fp32 accumulation, synthetic seeded data resident in HBM. One step = forward +
 fused multi-loss head + backward + gradient all-reduce (RCCL, N>1) + fused SGDM/L2/BN
 moving-average update. Weak scaling: 4 images per GPU at every N.
@@ -32,7 +33,7 @@ CLS_NAMES = {0: "conv_nt_kernel (forward implicit GEMM)", 1: "conv_nt_kernel (da
              2: "conv_wgrad_kernel (weight-gradient, split-K)"}
 
 
-def cpu_baseline(threads):
+def cpu_baseline(threads, pyramid):
     """Oracle (PyTorch-CPU fp32 restatement of the TF semantics) on a bounded sample:
     one 1024x2048 image, one full training step, after a 256x512 warm-up."""
     import numpy as np
@@ -40,17 +41,17 @@ def cpu_baseline(threads):
     from input_pipelines.synthetic import batch
     from oracle.tfseg import OracleNet, SegConfig, init_params
     torch.set_num_threads(threads)
-    warm = SegConfig(height=256, width=512, nb_pp=1, pyramid="psp")
+    warm = SegConfig(height=256, width=512, nb_pp=1, pyramid=pyramid)
     d = batch(1, 1, 0, 0, 256, 512)
     OracleNet(warm, init_params(warm), dtype=torch.float32).train_step(d["images"], d["px"])
-    cfg = SegConfig(height=H, width=W, nb_pp=1, pyramid="psp")
+    cfg = SegConfig(height=H, width=W, nb_pp=1, pyramid=pyramid)
     net = OracleNet(cfg, init_params(cfg), dtype=torch.float32)
     d = batch(2, 1, 0, 0, H, W)
     t = time.perf_counter()
     net.train_step(d["images"], d["px"])
     dt = time.perf_counter() - t
     return {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": "1 image 1024x2048, 1 full step (fwd+loss+bwd+SGDM), R50+PSP, fp32, "
+            "sample": f"1 image 1024x2048, 1 full step (fwd+loss+bwd+SGDM), R50+{pyramid.upper()}, fp32, "
                       f"oracle/tfseg.py on {threads} host threads ({dt:.1f} s)"}
 
 
@@ -60,6 +61,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--pyramid", default="aspp", choices=["aspp", "psp", "none"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -81,7 +83,7 @@ def main():
     from models.initializers import init_params
     from seg_hip import SegContext
 
-    ctx = SegContext(depth=50, pyramid="psp", height=H, width=W, nb_pp=NB, dtype=args.dtype,
+    ctx = SegContext(depth=50, pyramid=args.pyramid, height=H, width=W, nb_pp=NB, dtype=args.dtype,
                      device=local)
     ctx.load_params(init_params(ctx.param_info, seed=0))
     data = batch(1000 + rank, NB, 0, 0, H, W)
@@ -128,8 +130,19 @@ def main():
         r = cls[dom]
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
         achieved = r["gflop"] / r["ms"]  # GFLOP/ms == TFLOP/s
+        # HBM bytes per launch of that class from the committed PMC passes of this code
+        # (tools/pmc_traffic.sh + tools/pmc_traffic.py; rocprofv3 cannot run inside the bench)
+        traffic, tsrc = None, None
+        tpath = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+        if os.path.exists(tpath):
+            tj = json.load(open(tpath))
+            key = "conv_wgrad" if dom == 2 else "conv_nt"
+            if key in tj:
+                traffic = round(tj[key]["hbm_bytes_per_launch"])
+                tsrc = "profiles/r01_pmc_traffic.json (" + key + ", bytes per launch)"
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "traffic_source": tsrc,
                     "kernel": CLS_NAMES[dom],
                     "launches": r["launches"],
                     "avg_launch_ms": round(r["ms"] / max(r["launches"], 1), 4),
@@ -141,7 +154,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(threads=min(16, os.cpu_count() or 1))
+        cpu = cpu_baseline(threads=min(16, os.cpu_count() or 1), pyramid=args.pyramid)
 
     if rank == 0:
         value = world * NB * args.steps / elapsed
@@ -151,8 +164,9 @@ def main():
                "ms_per_step": round(elapsed * 1e3 / args.steps, 2),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": args.dtype, "data": "synthetic (seeded; random-init weights)",
-               "config": {"workload": "C2: ResNet-50 dilated OS8 + PSP, 1024x2048, per-pixel "
-                                      "CE multi-loss head, fwd+loss+bwd+allreduce+SGDM",
+               "config": {"workload": "C2: ResNet-50 dilated OS8 + " + args.pyramid.upper() +
+                                      ", 1024x2048, per-pixel CE multi-loss head, "
+                                      "fwd+loss+bwd+allreduce+SGDM",
                           "global_batch": world * NB, "per_gpu_batch": NB,
                           "image": [H, W], "parallelism": f"dp{world}"},
                "losses_last_step": [round(float(x), 5) for x in lv[:4]],

@@ -625,7 +625,14 @@ int build(seg_ctx* c) {
       c->pyr_conv.push_back(add_conv(c, std::string("feature_extractor/pyramid_module/") + nm[i], fd, fd, 1, 1, 1, false, true));
     c->pyr_final = add_conv(c, "feature_extractor/pyramid_module/Conv_4", 5 * fd, fd, 1, 1, 1, false, true);
   } else if (g.pyramid == SEG_PYRAMID_ASPP) {
-    return set_err(&c->err, -ENOTSUP, "ASPP pyramid not built in this version");
+    // the commented _create_aspp_module (hierarchical.py:209-226), in the PSP call site's scope
+    const std::string sc = "feature_extractor/pyramid_module/";
+    c->pyr_conv.push_back(add_conv(c, sc + "Conv", fd, fd, 1, 1, 1, false, true));     // image pool
+    c->pyr_conv.push_back(add_conv(c, sc + "Conv_1", fd, fd, 1, 1, 1, false, true));   // 1x1
+    const int rates[3] = {6, 12, 18};
+    for (int i = 0; i < 3; ++i)
+      c->pyr_conv.push_back(add_conv(c, sc + "Conv_" + std::to_string(i + 2), fd, fd, 3, 1, rates[i], false, true));
+    c->pyr_final = add_conv(c, sc + "Conv_5", 5 * fd, fd, 1, 1, 1, false, true);
   }
   const char* hn[3] = {"l1", "l2_vehicle", "l2_human"};
   for (int h = 0; h < 3; ++h)
@@ -706,6 +713,28 @@ int build(seg_ctx* c) {
       gp = std::max(gp, (size_t)N * Hf * kc * fd);
     }
     if (int r = dalloc(c, &c->grid_part, gp)) return r;
+    if (int r = alloc_conv(c, c->convs[c->pyr_final], N, Hf, Wf)) return r;
+    if (int r = alloc_relu_act(c, c->feat, N, Hf, Wf, fd)) return r;
+    if (int r = alloc_act(c, c->dfeat, N, Hf, Wf, fd)) return r;
+  } else if (g.pyramid == SEG_PYRAMID_ASPP) {
+    if (int r = alloc_relu_act(c, c->z_dfd, N, Hf, Wf, fd)) return r;
+    if (int r = alloc_act(c, c->concat, N, Hf, Wf, 5 * fd)) return r;
+    if (int r = alloc_act(c, c->dconcat, N, Hf, Wf, 5 * fd)) return r;
+    std::vector<std::pair<int, int>> win{{Hf, Wf}};   // global average pool
+    if (int r = make_pool_grids(c, c->pool_grids, Hf, Wf, win)) return r;
+    Act pa, dpa, za, dza;
+    if (int r = alloc_act(c, pa, N, 1, 1, fd)) return r;
+    if (int r = alloc_act(c, dpa, N, 1, 1, fd)) return r;
+    if (int r = alloc_act(c, za, N, 1, 1, fd)) return r;
+    if (int r = alloc_act(c, dza, N, 1, 1, fd)) return r;
+    c->pooled.push_back(pa); c->dpooled.push_back(dpa); c->zb.push_back(za); c->dzb.push_back(dza);
+    if (int r = alloc_conv(c, c->convs[c->pyr_conv[0]], N, 1, 1)) return r;
+    GridSpec ug;
+    if (int r = make_resize_grid(c, ug, 1, 1, Hf, Wf)) return r;
+    c->up_grids.push_back(ug);
+    if (int r = dalloc(c, &c->grid_part, (size_t)N * Hf * fd)) return r;
+    for (int b = 1; b < 5; ++b)
+      if (int r = alloc_conv(c, c->convs[c->pyr_conv[b]], N, Hf, Wf)) return r;
     if (int r = alloc_conv(c, c->convs[c->pyr_final], N, Hf, Wf)) return r;
     if (int r = alloc_relu_act(c, c->feat, N, Hf, Wf, fd)) return r;
     if (int r = alloc_act(c, c->dfeat, N, Hf, Wf, fd)) return r;
@@ -847,6 +876,26 @@ int forward(Step& S, const float* images) {
     }
     if (int r = conv_forward(S, c->pyr_final, c->concat)) return r;
     if (int r = bn_apply(S, c->pyr_final, c->feat, 0)) return r;
+  } else if (c->cfg.pyramid == SEG_PYRAMID_ASPP) {
+    const Act& z = c->z_dfd;
+    const int fd = c->cfg.feature_dims;
+    // image-pool branch: global mean -> 1x1 conv/BN/ReLU -> align-corners broadcast (slice 0)
+    HIPCALL(c, launch_grid_rowreduce(S.dt, z.p, z.N, z.H, z.W, z.C, z.ld, c->pool_grids,
+                                     c->grid_part, S.s));
+    void* outs[SEG_MAX_GRIDS] = {c->pooled[0].p, nullptr, nullptr, nullptr};
+    HIPCALL(c, launch_grid_colreduce(S.dt, c->grid_part, z.N, z.H, z.W, z.C, c->pool_grids, outs, S.s));
+    if (int r = conv_forward(S, c->pyr_conv[0], c->pooled[0])) return r;
+    if (int r = bn_apply(S, c->pyr_conv[0], c->zb[0], 0)) return r;
+    Act d0 = slice(c, c->concat, 0, fd);
+    HIPCALL(c, launch_resize_fwd(S.dt, c->zb[0].p, c->zb[0].N, 1, 1, fd, c->zb[0].ld, d0.p, d0.H,
+                                 d0.W, d0.ld, S.s));
+    // 1x1 and the rate-6/12/18 3x3 branches write their BN/ReLU outputs into slices 1..4
+    for (int b = 1; b < 5; ++b) {
+      if (int r = conv_forward(S, c->pyr_conv[b], z)) return r;
+      if (int r = bn_apply(S, c->pyr_conv[b], slice(c, c->concat, b * fd, fd), 0)) return r;
+    }
+    if (int r = conv_forward(S, c->pyr_final, c->concat)) return r;
+    if (int r = bn_apply(S, c->pyr_final, c->feat, 0)) return r;
   }
   for (int h = 0; h < 3; ++h) {
     if (int r = unit_forward(S, c->heads[h])) return r;
@@ -887,6 +936,32 @@ int backward(Step& S) {
     Act d0 = slice(c, c->dconcat, 0, fd);
     HIPCALL(c, launch_psp_input_bwd(S.dt, d0.p, d0.ld, c->pool_grids, dps, d0.N, d0.H, d0.W, fd,
                                     c->dz_dfd.p, c->dz_dfd.ld, S.s));
+  } else if (c->cfg.pyramid == SEG_PYRAMID_ASPP) {
+    const int fd = c->cfg.feature_dims;
+    if (int r = bn_backward(S, c->pyr_final, c->dfeat, 0, &c->feat, nullptr)) return r;
+    if (int r = conv_wgrad(S, c->pyr_final, c->concat)) return r;
+    if (int r = conv_dgrad(S, c->pyr_final, c->dconcat)) return r;
+    // image-pool branch: transpose of the broadcast = sum over the map
+    Act s0 = slice(c, c->dconcat, 0, fd);
+    HIPCALL(c, launch_grid_rowreduce(S.dt, s0.p, s0.N, s0.H, s0.W, fd, s0.ld, c->up_grids[0],
+                                     c->grid_part, S.s));
+    void* outs[SEG_MAX_GRIDS] = {c->dzb[0].p, nullptr, nullptr, nullptr};
+    HIPCALL(c, launch_grid_colreduce(S.dt, c->grid_part, s0.N, s0.H, s0.W, fd, c->up_grids[0], outs, S.s));
+    if (int r = bn_backward(S, c->pyr_conv[0], c->dzb[0], 0, &c->zb[0], nullptr)) return r;
+    if (int r = conv_wgrad(S, c->pyr_conv[0], c->pooled[0])) return r;
+    if (int r = conv_dgrad(S, c->pyr_conv[0], c->dpooled[0])) return r;
+    // conv branches: dz_dfd = sum of their data gradients (fixed branch order)
+    for (int b = 1; b < 5; ++b) {
+      Act db = slice(c, c->dconcat, b * fd, fd);
+      Act zb = slice(c, c->concat, b * fd, fd);
+      if (int r = bn_backward(S, c->pyr_conv[b], db, 0, &zb, nullptr)) return r;
+      if (int r = conv_wgrad(S, c->pyr_conv[b], c->z_dfd)) return r;
+      if (int r = conv_dgrad(S, c->pyr_conv[b], c->dz_dfd, b > 1 ? &c->dz_dfd : nullptr)) return r;
+    }
+    // + the global-average-pool transpose, in place
+    const void* dps[SEG_MAX_GRIDS] = {c->dpooled[0].p, nullptr, nullptr, nullptr};
+    HIPCALL(c, launch_psp_input_bwd(S.dt, c->dz_dfd.p, c->dz_dfd.ld, c->pool_grids, dps, c->dz_dfd.N,
+                                    c->dz_dfd.H, c->dz_dfd.W, fd, c->dz_dfd.p, c->dz_dfd.ld, S.s));
   }
   if (int r = bn_backward(S, c->dfd, c->dz_dfd, 0, &c->z_dfd, nullptr)) return r;
   if (int r = conv_wgrad(S, c->dfd, c->units.back().out)) return r;

@@ -51,7 +51,9 @@ def get_context(config, params, device=None):
     import torch
     nb_pp, nb_pb, nb_pi = sub_batches(config, params)
     depth = 101 if getattr(params, 'name_feature_extractor', 'resnet_v1_50') == 'resnet_v1_101' else 50
-    pyramid = getattr(params, 'pyramid', None) or ('psp' if getattr(params, 'psp_module', False) else 'none')
+    pyramid = getattr(params, 'pyramid', None) or (
+        'psp' if getattr(params, 'psp_module', False) else
+        'aspp' if getattr(params, 'aspp_module', False) else 'none')
     dev = torch.cuda.current_device() if device is None else device
     key = (dev, depth, pyramid, params.height_feature_extractor, params.width_feature_extractor,
            nb_pp, nb_pb, nb_pi, getattr(params, 'compute_dtype', 'bf16'),
@@ -112,5 +114,8 @@ def add_model_arguments(argparser):
     a('--batch_norm_accumulate_statistics', action='store_true')
     a('--batch_norm_decay', type=float, default=0.9)
     # build-side additions
+    # ASPP: the reference's commented-out _create_aspp_module (hierarchical.py:209-226), built
+    # in the PSP call site's 'pyramid_module' scope; mutually exclusive with --psp_module
+    a('--aspp_module', action='store_true')
     a('--compute_dtype', type=str, default='bf16', choices=['bf16', 'fp32'])
     a('--init_seed', type=int, default=0)

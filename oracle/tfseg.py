@@ -144,12 +144,13 @@ def build_specs(cfg: SegConfig) -> List[ConvSpec]:
                                   fd, fd, 1))
         specs.append(ConvSpec("feature_extractor/pyramid_module/Conv_4", 5 * fd, fd, 1))
     elif cfg.pyramid == "aspp":
-        # build-side: the commented spec at hierarchical.py:209-226
-        specs.append(ConvSpec("feature_extractor/aspp_module/Conv", fd, fd, 1))       # image pool
-        specs.append(ConvSpec("feature_extractor/aspp_module/Conv_1", fd, fd, 1))     # 1x1
+        # the commented spec at hierarchical.py:209-226, called where _create_psp_module is
+        # (:55-57, variable scope 'pyramid_module'); slim names convs in creation order
+        specs.append(ConvSpec("feature_extractor/pyramid_module/Conv", fd, fd, 1))    # image pool
+        specs.append(ConvSpec("feature_extractor/pyramid_module/Conv_1", fd, fd, 1))  # 1x1
         for i, r in enumerate((6, 12, 18)):
-            specs.append(ConvSpec(f"feature_extractor/aspp_module/Conv_{i + 2}", fd, fd, 3, 1, r))
-        specs.append(ConvSpec("feature_extractor/aspp_module/Conv_5", 5 * fd, fd, 1))
+            specs.append(ConvSpec(f"feature_extractor/pyramid_module/Conv_{i + 2}", fd, fd, 3, 1, r))
+        specs.append(ConvSpec("feature_extractor/pyramid_module/Conv_5", 5 * fd, fd, 1))
     for head in ("l1_features", "l2_vehicle_features", "l2_human_features"):
         specs += _bottleneck_specs(f"adaptation_module/{head}", fd, fd, fd, 1, 1)
     c1, c2, c3 = n_classes(cfg.dataset)
@@ -375,12 +376,12 @@ class OracleNet:
         """ASPP per the commented spec (hierarchical.py:209-226); build-side, unpinned."""
         h, w = x.shape[2], x.shape[3]
         pooled = F.avg_pool2d(x, (h, w), stride=(h, w))
-        c = self.conv_bn(pooled, "feature_extractor/aspp_module/Conv", record=record)
+        c = self.conv_bn(pooled, "feature_extractor/pyramid_module/Conv", record=record)
         br = [resize_bilinear_ac(c, h, w),
-              self.conv_bn(x, "feature_extractor/aspp_module/Conv_1", record=record)]
+              self.conv_bn(x, "feature_extractor/pyramid_module/Conv_1", record=record)]
         for i in range(3):
-            br.append(self.conv_bn(x, f"feature_extractor/aspp_module/Conv_{i + 2}", record=record))
-        return self.conv_bn(torch.cat(br, 1), "feature_extractor/aspp_module/Conv_5", record=record)
+            br.append(self.conv_bn(x, f"feature_extractor/pyramid_module/Conv_{i + 2}", record=record))
+        return self.conv_bn(torch.cat(br, 1), "feature_extractor/pyramid_module/Conv_5", record=record)
 
     # -- forward -------------------------------------------------------------------------
     def forward(self, images_nhwc, record=None):

@@ -70,6 +70,7 @@ CONFIGS = [
     SegConfig(height=64, width=96, nb_pp=1, nb_pb=1, nb_pi=1, pyramid="psp"),
     SegConfig(height=48, width=64, nb_pp=1, pyramid="none"),
     SegConfig(depth=101, height=48, width=64, nb_pp=1, nb_pb=1, pyramid="psp"),
+    SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp"),
 ]
 
 
@@ -119,7 +120,8 @@ def test_train_step_fp32(cuda, cfg):
             assert _rel(nat["params"][k], v.detach().numpy().reshape(-1)) < 1e-3, k
 
 
-def test_bf16_layerwise(cuda):
+@pytest.mark.parametrize("pyramid", ["psp", "aspp"])
+def test_bf16_layerwise(cuda, pyramid):
     """bf16 storage / fp32 accumulation, layer by layer.
 
     End-to-end bf16-vs-fp64 comparison is meaningless at random init: the network is chaotic
@@ -129,10 +131,10 @@ def test_bf16_layerwise(cuda):
     from input_pipelines.synthetic import batch
     from oracle.tfseg import build_specs, conv_tf
     from seg_hip import SegContext
-    cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="psp")
+    cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid=pyramid)
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=5).items()}
     data = batch(12, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
-    ctx = SegContext(pyramid="psp", height=64, width=128, nb_pp=1, nb_pb=1, dtype="bf16")
+    ctx = SegContext(pyramid=pyramid, height=64, width=128, nb_pp=1, nb_pb=1, dtype="bf16")
     ctx.load_params(params)
     ctx.forward(torch.as_tensor(data["images"]).to(cuda))
     ctx.loss(torch.as_tensor(data["px"]).to(cuda), torch.as_tensor(data["bbox"]).to(cuda))
