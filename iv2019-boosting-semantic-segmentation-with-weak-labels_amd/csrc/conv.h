@@ -56,12 +56,13 @@ int conv_nt_mtiles(long M);  // upper bound on BN-stat partial tiles (128-row ti
 // rows per BN-stat partial tile of the kernel launch_conv_nt will pick (128 or 256)
 int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a);
 bool conv_nt_v2_ok(const ConvArgs& a);
+int conv_nt_v2_rows(const ConvArgs& a);   // tile rows (= BN-stat partial rows) of the v2 config
 // true when launch_conv_nt runs the v2 kernel
 bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a);
 hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s);
 bool conv_wgrad_v2_ok(const WgradArgs& a);
 hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s);
-void conv_wgrad_v2_tile(int Co, int Ncol, int* bm, int* bn);
+void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn);
 
 // 3-channel stem in bf16, laid out as 8-channel taps (tap8 mode):
 //   images f32 [M][3] -> bf16 [M][8] (channels 3..7 zero)

@@ -616,7 +616,7 @@ hipError_t wg_dispatch(const WgradArgs& a, hipStream_t s) {
 int conv_nt_mtiles(long M) { return ceil_div(M, 128); }
 
 int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a) {
-  return (dtype == SEG_BF16 && !out_f32 && conv_nt_v2_ok(a)) ? 256 : 128;
+  return (dtype == SEG_BF16 && !out_f32 && conv_nt_v2_ok(a)) ? conv_nt_v2_rows(a) : 128;
 }
 
 namespace {

@@ -14,6 +14,7 @@
 //    store per 8 outputs, and the per-column BN partial statistics (sum, M2 about the tile
 //    mean) for the fused batch-norm.
 #include "conv.h"
+#include <algorithm>
 
 #ifndef SEG_MFMA_PRIO
 #define SEG_MFMA_PRIO 1   // s_setprio(1) around MFMA clusters (+1-2 % measured)
@@ -65,10 +66,10 @@ template <> struct AccOf<16> { typedef f32x4_t T; static constexpr int N = 4; };
 // MF: MFMA shape (16: v_mfma_f32_16x16x32_bf16). A v_mfma_f32_32x32x16_bf16 main loop with
 // fragments double-buffered across k16-steps was measured 5-9 % slower on the C2 layer shapes
 // and removed; the epilogue keeps the shape-generic (row_of / col_of) accumulator walk.
-template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16>
-__global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
+template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM_ = 256>
+__global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_kernel(ConvArgs a) {
   const bf16_t* zero = g_zero16;
-  constexpr int BM = 256;
+  constexpr int BM = BM_;
   constexpr int WM = BM / WMW, WN = BN / WNW;
   constexpr int FM = WM / MF, FN = WN / MF;
   constexpr int NA = AccOf<MF>::N;   // accumulator elements per lane per fragment
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
           t.x += u.x;
           nt += (float)WM;
         }
-        if (n0 + c < a.Co)   // one (sum, M2) per 256-row tile (conv_nt_stat_rows)
+        if (n0 + c < a.Co)   // one (sum, M2) per BM-row tile (conv_nt_stat_rows)
           *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = t;
       }
     }
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
         float t = 0.f;
 #pragma unroll
         for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
-        if (n0 + c < a.Co)   // one (sum, M2) per 256-row tile (conv_nt_stat_rows)
+        if (n0 + c < a.Co)   // one (sum, M2) per BM-row tile (conv_nt_stat_rows)
           *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = make_float2(tot[j], t);
       }
     }
@@ -416,14 +417,13 @@ __global__ __launch_bounds__(V2_THREADS, 1) void conv_nt_v2_kernel(ConvArgs a) {
   }
 }
 
-template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16>
+template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM = 256>
 hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
-  constexpr int BM = 256;
   constexpr int STAGE_BYTES = (BM + BN) * 128;
-  constexpr int EPI = BM * (64 + 4) * 4 + 64 * 8 * 8 * 4;
+  constexpr int EPI = BM * (64 + 4) * 4;
   constexpr int LDS = STAGES * STAGE_BYTES > EPI ? STAGES * STAGE_BYTES : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST, T8, MF>;
+  auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST, T8, MF, BM>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -445,6 +445,14 @@ bool conv_nt_v2_ok(const ConvArgs& a) {
            a.ldw >= (a.KH * a.KW * 8 + BK - 1) / BK * BK && (a.ldw % 8) == 0 && !a.r && !a.r2;
   return (a.st == 1 || a.st == 2) && (a.C % BK) == 0 && (a.ldx % 8) == 0 && (a.ldw % 8) == 0 && (a.Co % 8) == 0 &&
          (a.ldy % 8) == 0 && (!a.r || a.ldr % 8 == 0) && (!a.r2 || a.ldr2 % 8 == 0);
+}
+
+// rows per tile of the v2 config launch_conv_nt_v2 picks (= BN-statistics partial rows).
+// (Measured and rejected: 128 x 128 tiles with a 64 KB ring, two workgroups per CU, for short
+// reductions K <= 512 -- 10-20 % slower than 256-row tiles on the C2 1x1 layers.)
+int conv_nt_v2_rows(const ConvArgs& a) {
+  (void)a;
+  return 256;
 }
 
 template <int ST>
@@ -694,16 +702,27 @@ bool conv_wgrad_v2_ok(const WgradArgs& a) {
          (long)a.N * a.Ho * a.Wo < (1L << 31);
 }
 
-// tile (BM co x BN cols): the largest the extents fill. 256 x 256 (wave tiles 128 x 64) keeps
-// LDS fragment traffic below the MFMA time and halves L2 re-reads vs 128 x 256.
-void conv_wgrad_v2_tile(int Co, int Ncol, int* bm, int* bn) {
-  *bm = Co <= 64 ? 64 : (Co <= 128 ? 128 : 256);
-  *bn = Ncol <= 64 ? 64 : (Ncol <= 128 ? 128 : 256);
+// tile (BM co x BN cols): the largest the extents fill -- 256 x 256 (wave tiles 128 x 64)
+// keeps LDS fragment traffic below the MFMA time and halves L2 re-reads vs 128 x 256 -- then
+// halved (larger side first) while tiles x pixel splits would leave CUs idle (small outputs
+// such as 256 x 256 1x1 convs: 1 tile x 64 splits = 64 workgroups otherwise)
+void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn) {
+  int m = Co <= 64 ? 64 : (Co <= 128 ? 128 : 256);
+  int n = Ncol <= 64 ? 64 : (Ncol <= 128 ? 128 : 256);
+  const long maxs = std::min<long>(256, std::max<long>(1, P / 2048));
+  auto blocks = [&]() { return (long)((Co + m - 1) / m) * ((Ncol + n - 1) / n) * maxs; };
+  while (blocks() < 256) {
+    if (m >= n && m > 64) m /= 2;
+    else if (n > 64) n /= 2;
+    else break;
+  }
+  *bm = m;
+  *bn = n;
 }
 
 hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s) {
   int bm, bn;
-  conv_wgrad_v2_tile(a.Co, a.KH * a.KW * a.C, &bm, &bn);
+  conv_wgrad_v2_tile(a.Co, a.KH * a.KW * a.C, (long)a.N * a.Ho * a.Wo, &bm, &bn);
   if (bm == 64) {
     if (bn == 64) return wg2_launch<64, 64, 4, 2, 3>(a, s);
     if (bn == 128) return wg2_launch<64, 128, 2, 4, 3>(a, s);

@@ -344,9 +344,9 @@ int wgrad_splits(const ConvL& L, int ci = 0) {
   if (!ci) ci = L.ci;   // 8 for the tap8 stem
   int BM = L.co_pad <= 64 ? 64 : 128;
   int BN = 128;
-  if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, L.k * L.k * ci, &BM, &BN);
-  long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * ci + BN - 1) / BN);
   long P = (long)L.N * L.Ho * L.Wo;
+  if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, L.k * L.k * ci, P, &BM, &BN);
+  long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * ci + BN - 1) / BN);
   // ~2 waves of 256 single-workgroup CUs, each split >= 32 K-steps of 64 pixels
   long s = std::max<long>(1, 512 / std::max<long>(tiles, 1));
   long maxs = std::max<long>(1, P / 2048);
@@ -1290,9 +1290,9 @@ int seg_op_conv_fwd(int dtype, const void* x, int N, int H, int W, int C, int ld
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_fwd");
 }
 
-int seg_op_conv_stat_rows(int dtype, int C, int ldx, int Co, int ldy) {
+int seg_op_conv_stat_rows(int dtype, int C, int ldx, int Co, int ldy, int k) {
   ConvArgs a{};
-  a.C = C; a.ldx = ldx; a.Co = Co; a.ldy = ldy; a.ldw = 8; a.st = 1;
+  a.C = C; a.ldx = ldx; a.Co = Co; a.ldy = ldy; a.ldw = 8; a.st = 1; a.KH = a.KW = k;
   return conv_nt_stat_rows(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, 0, a);
 }
 

@@ -19,6 +19,7 @@ CASES = [
     (1, 37, 45, 3, 64, 7, 2, 1, True),        # stem (generic small-C path)
     (2, 9, 10, 256, 14, 1, 1, 1, False),      # logits (Co=14)
     (1, 6, 6, 1280, 256, 1, 1, 1, False),     # PSP final (C=1280)
+    (2, 15, 21, 256, 512, 1, 1, 1, False),    # short K, wide N: 128-row tiles, 2 per CU
 ]
 
 
@@ -78,7 +79,7 @@ def test_conv_fwd(cuda, dtype, case):
     tol = 1e-4 if dtype == "fp32" else 2e-2
     assert _rel(y, ref) < tol
     # BN partial statistics: merge (sum, M2 about the tile mean) and compare
-    tr = LIB.seg_op_conv_stat_rows(1 if dtype == "bf16" else 0, Ci, Ci, Co, Co)
+    tr = LIB.seg_op_conv_stat_rows(1 if dtype == "bf16" else 0, Ci, Ci, Co, Co, k)
     nt = (M + tr - 1) // tr
     st = stats.cpu().numpy().astype(np.float64)[:nt]
     cnt = np.minimum(tr, M - np.arange(nt) * tr).astype(np.float64)

@@ -8,7 +8,8 @@ from input_pipelines.synthetic import batch
 from models.initializers import init_params
 from seg_hip import SegContext
 H, W, NB = 1024, 2048, 4
-ctx = SegContext(depth=50, pyramid="psp", height=H, width=W, nb_pp=NB, dtype="bf16")
+PYR = os.environ.get("PYRAMID", "aspp")
+ctx = SegContext(depth=50, pyramid=PYR, height=H, width=W, nb_pp=NB, dtype="bf16")
 ctx.load_params(init_params(ctx.param_info, seed=0))
 d = batch(1000, NB, 0, 0, H, W)
 img = torch.as_tensor(d["images"]).cuda(); px = torch.as_tensor(d["px"]).cuda()
@@ -24,6 +25,11 @@ tot = collections.defaultdict(float)
 for r in rows:
     tot[r["cls"]] += r["ms"]
 print("class totals ms:", dict(tot))
+os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+with open(os.path.join(REPO, "gpurun_out", "layers.csv"), "w") as f:
+    f.write("cls,name,ci,co,k,rate,ho,wo,gflop,ms\n")
+    for r in rows:
+        f.write("%d,%s,%d,%d,%d,%d,%d,%d,%.4f,%.5f\n" % (r["cls"], r["name"], r["ci"], r["co"], r["k"], r["rate"], r["ho"], r["wo"], r["gflop"], r["ms"]))
 rows.sort(key=lambda r: -r["ms"])
 bn = [r for r in rows if r["cls"] >= 3]
 for k in (3, 4, 5):

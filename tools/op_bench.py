@@ -12,6 +12,9 @@ SHAPES = {  # N, H, W, Ci, Co, k, stride, rate
     "b4c3": (4, 128, 256, 512, 2048, 1, 1, 1),
     "b4c1": (4, 128, 256, 2048, 512, 1, 1, 1),
     "b3c2": (4, 128, 256, 256, 256, 3, 1, 2),
+    "b3c1": (4, 128, 256, 1024, 256, 1, 1, 1),
+    "b3c3": (4, 128, 256, 256, 1024, 1, 1, 1),
+    "head1": (4, 128, 256, 256, 256, 1, 1, 1),
 }
 op = sys.argv[1] if len(sys.argv) > 1 else "wgrad"
 N, H, W, Ci, Co, k, s, r = SHAPES[sys.argv[2] if len(sys.argv) > 2 else "b4c2"]
