@@ -60,6 +60,10 @@ int conv_nt_v2_rows(const ConvArgs& a);   // tile rows (= BN-stat partial rows) 
 // true when launch_conv_nt runs the v2 kernel
 bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a);
 hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s);
+// ping-pong 256x256 main loop (conv_pp.hip) for the v2 cases with Co > 128
+bool conv_nt_pp_ok(const ConvArgs& a);
+bool conv_nt_pp_enabled();
+hipError_t launch_conv_nt_pp(const ConvArgs& a, hipStream_t s);
 bool conv_wgrad_v2_ok(const WgradArgs& a);
 hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s);
 void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn);

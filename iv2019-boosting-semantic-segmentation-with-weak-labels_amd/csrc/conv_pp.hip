@@ -1,0 +1,461 @@
+// bf16 implicit-GEMM convolution, forward + data-gradient, "ping-pong" schedule for gfx950.
+//
+// Same operands, gather and epilogue as conv_nt_v2_kernel (conv_v2.hip), different main loop:
+//
+//  * 256 x 256 tile, 8 waves as 2 (M) x 4 (N), each wave owns 128 rows x 64 columns split in
+//    four 64 x 32 quadrants;
+//  * every 64-deep K-tile is four PHASES, one per quadrant, in the order (qm,qn) = (0,0),
+//    (0,1), (1,1), (1,0); a phase is a LOAD segment (the ds_read_b128 fragments the quadrant
+//    needs that are not already in registers, plus one half-tile of LDS-DMA for the next
+//    K-tile) and an MFMA segment (16 x v_mfma_f32_16x16x32_bf16), separated by s_barrier;
+//  * the two wave rows are staggered by one barrier (wave row 1 starts with an extra
+//    s_barrier), so on every SIMD one wave is in its MFMA segment while the other issues its
+//    LDS reads and DMA: the matrix pipe does not idle across barriers;
+//  * LDS holds two K-tile buffers, each four 16 KB half-tiles (A rows 0-127 / 128-255, B rows
+//    0-127 / 128-255). Phase i of K-tile k refills half ORDER[i] = A0, B0, B1, A1 of K-tile
+//    k+1 in the other buffer; every half is restaged >= 2 segments after its last ds_read
+//    (WAR) and waited for with a counted vmcnt before the barrier that precedes its first
+//    read (RAW): vmcnt(4) after phases 0, 1 and 3 (two later half-tiles = 4 DMAs per lane
+//    stay in flight), none after phase 2;
+//  * operands are fetched with buffer_load ... lds through buffer resources: a 32-bit byte
+//    offset per lane, padding taps and rows past the tensor given an out-of-range offset so
+//    the buffer unit writes zeros (4 VALU per A DMA, 1 per B DMA: the load segment is short);
+//  * K-tiles run channel-chunk-major, tap-minor, so the KH*KW shifted reads of one chunk's
+//    source rows hit L2 (dilated 3x3: +6 %).
+#include "conv.h"
+
+namespace {
+
+constexpr int PP_THREADS = 512;
+constexpr int PBK = 64;                    // bf16 K-elements per K-tile (128-B LDS rows)
+constexpr int HALF = 128 * 128;            // one half-tile: 128 rows x 128 B
+constexpr int BUF = 4 * HALF;              // A0 A1 B0 B1
+constexpr int PP_LDS = 2 * BUF;            // 128 KB
+constexpr int EPI_COLS = 64, EPI_LD = EPI_COLS + 4;
+
+__device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+
+// compiler fences around the raw barrier: nothing moves across it (IR or machine schedule)
+__device__ __forceinline__ void pp_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+template <int ST>
+__device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
+  constexpr int BM = 256, BN = 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;   // wm = wave row = ping-pong group
+  const int lr = lane & 15, lq = lane >> 4;
+  const long M = (long)a.N * a.Ho * a.Wo;
+  const int mtiles = (int)((M + BM - 1) / BM);
+  const int ntiles = (a.Co + BN - 1) / BN;
+  const int nwg = mtiles * ntiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int mt = wg / ntiles, nt = wg - mt * ntiles;
+  const long m0 = (long)mt * BM;
+  const int n0 = nt * BN;
+  const int nk = (a.KH * a.KW * a.C) / PBK;
+  const int ntaps = a.KH * a.KW;
+  const bf16_t* X = (const bf16_t*)a.x;
+  const bf16_t* Wt = (const bf16_t*)a.w;
+
+  // ---- operand addressing: buffer resources, 32-bit byte offsets per lane ----
+  // Out-of-range taps and rows get the offset OOB (>= num_records): the buffer unit returns
+  // zeros, so the LDS image is written whole with no zero-source select. The host guarantees
+  // both operands are < 2^31 bytes.
+  constexpr uint32_t OOB = 0x80000000u;
+  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0,
+                                                      (int)((long)a.N * a.H * a.W * a.ldx * 2), 0x00020000);
+  const auto rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (int)((long)a.Co * a.ldw * 2), 0x00020000);
+  // A rows: half h, DMA instruction i -> tile row h*128 + (i*8+wave)*8 + lane/8 (j = h*2 + i).
+  // ST == 1: byte offset of the tap-(0,0) source and a validity mask, bit kh (0-3) for the row
+  // and bit 4+kw for the column of every tap; ST == 2 (transposed gather) decodes per tap.
+  const int pc = lane & 7;
+  int a_voff[4], a_bits[4], a_h0[4], a_w0[4], a_lc[4];
+  long a_nb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
+    const int row = (j >> 1) * 128 + rr;
+    a_lc[j] = swz(rr, pc);
+    const long m = m0 + row;
+    const bool ok = m < M;
+    const long mm = ok ? m : 0;
+    const int wo = (int)(mm % a.Wo);
+    const long t = mm / a.Wo;
+    const int ho = (int)(t % a.Ho);
+    a_nb[j] = (t / a.Ho) * a.H;
+    a_h0[j] = ok ? ho * a.sf - a.pad_h : -(1 << 28);
+    a_w0[j] = wo * a.sf - a.pad_w;
+    a_voff[j] = (((int)(a_nb[j] + a_h0[j]) * a.W + a_w0[j]) * a.ldx + a_lc[j] * 8) * 2;
+    int bits = 0;
+    for (int q = 0; q < a.KH; ++q) bits |= ((unsigned)(a_h0[j] + q * a.dil) < (unsigned)a.H) << q;
+    for (int q = 0; q < a.KW; ++q) bits |= ((unsigned)(a_w0[j] + q * a.dil) < (unsigned)a.W) << (4 + q);
+    a_bits[j] = bits;
+  }
+  // B rows: half g, instruction i -> output channel n0 + g*128 + (i*8+wave)*8 + lane/8
+  uint32_t b_voff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
+    const int co = n0 + (j >> 1) * 128 + rr;
+    b_voff[j] = co < a.Co ? (uint32_t)((co * a.ldw + swz(rr, pc) * 8) * 2) : OOB;
+  }
+
+  // per-K-tile wave-uniform decode. K-tile order: channel chunk outer, tap inner, so the
+  // KH*KW shifted reads of one chunk's source rows follow each other while they are in L2
+  struct KT { int need, s_tap2, k02, dh, dw, c0; };
+  int nx_tap = 0, nx_c0 = 0;   // (tap, chunk) of the next K-tile to decode, stepped in order
+  auto ktile_next = [&]() {
+    KT t;
+    const int tap = nx_tap;
+    t.c0 = nx_c0;
+    if (++nx_tap == ntaps) { nx_tap = 0; nx_c0 += PBK; }
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    t.dh = kh * a.dil;
+    t.dw = kw * a.dil;
+    t.need = (1 << kh) | (16 << kw);
+    t.s_tap2 = ((t.dh * a.W + t.dw) * a.ldx + t.c0) * 2;
+    t.k02 = (tap * a.C + t.c0) * 2;   // weight column, bytes
+    return t;
+  };
+
+  // half ids: 0 = A0, 1 = A1, 2 = B0, 3 = B1 (LDS offset hid * HALF inside a K-tile buffer)
+  auto issue_half = [&](int kb, const KT& t, int hid) {
+    char* dst = smem + (kb & 1) * BUF + hid * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      auto* ldst = (__attribute__((address_space(3))) void*)(dst + (i * 8 + wave) * 1024);
+      if (hid < 2) {
+        const int j = hid * 2 + i;
+        uint32_t off;
+        if constexpr (ST == 1) {
+          off = (a_bits[j] & t.need) == t.need ? (uint32_t)(a_voff[j] + t.s_tap2) : OOB;
+        } else {
+          int hi = a_h0[j] + t.dh, wi = a_w0[j] + t.dw;
+          bool ok = (hi >= 0) & (wi >= 0) & ((hi % ST) == 0) & ((wi % ST) == 0);
+          hi /= ST;
+          wi /= ST;
+          ok &= (hi < a.H) & (wi < a.W);
+          off = ok ? (uint32_t)(((int)((a_nb[j] + hi) * a.W + wi) * a.ldx + t.c0 + a_lc[j] * 8) * 2) : OOB;
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, ldst, 16, off, 0, 0, 0);
+      } else {
+        const int j = (hid - 2) * 2 + i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, ldst, 16, b_voff[j] + t.k02, 0, 0, 0);
+      }
+    }
+  };
+
+  f32x4_t acc[2][2][4][2];   // [qm][qn][fi][fj]
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t af[4][2], bfr[2][2];   // [frag][k-half]
+  auto read_a = [&](const char* buf, int qm) {
+    const char* A = buf + qm * HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + lr;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) af[i][s] = *(const bf16x8_t*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
+    }
+  };
+  auto read_b = [&](const char* buf, int qn) {
+    const char* B = buf + (2 + qn) * HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = wn * 32 + j * 16 + lr;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) bfr[j][s] = *(const bf16x8_t*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
+    }
+  };
+  auto mfma_q = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[qm][qn][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- prologue: K-tile 0, halves in issue order A0, B0, B1, A1 ----
+  {
+    const KT t0 = ktile_next();
+    issue_half(0, t0, 0);
+    issue_half(0, t0, 2);
+    issue_half(0, t0, 3);
+    issue_half(0, t0, 1);
+  }
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A0, B0 landed (B1, A1 in flight)
+  pp_barrier();
+  if (wm == 1) pp_barrier();   // stagger: wave row 1 runs one segment behind
+
+  // wait after a phase for the halves the next phase reads first (see header)
+  auto wait_next = [&](bool more) {
+    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  for (int kb = 0; kb < nk; ++kb) {
+    const char* buf = smem + (kb & 1) * BUF;
+    const bool more = kb + 1 < nk;
+    const KT tn = ktile_next();   // K-tile kb + 1
+    // phase 0: quadrant (0,0), needs A0 + B0; refill A0 of kb+1
+    read_a(buf, 0);
+    read_b(buf, 0);
+    if (more) issue_half(kb + 1, tn, 0);
+    if (wm == 1) wait_next(more);
+    pp_barrier();
+    mfma_q(0, 0);
+    if (wm == 0) wait_next(more);
+    pp_barrier();
+    // phase 1: quadrant (0,1), needs B1; refill B0
+    read_b(buf, 1);
+    if (more) issue_half(kb + 1, tn, 2);
+    if (wm == 1) wait_next(more);
+    pp_barrier();
+    mfma_q(0, 1);
+    if (wm == 0) wait_next(more);
+    pp_barrier();
+    // phase 2: quadrant (1,1), needs A1; refill B1
+    read_a(buf, 1);
+    if (more) issue_half(kb + 1, tn, 3);
+    pp_barrier();
+    mfma_q(1, 1);
+    pp_barrier();
+    // phase 3: quadrant (1,0), needs B0; refill A1
+    read_b(buf, 0);
+    if (more) issue_half(kb + 1, tn, 1);
+    if (more && wm == 1) wait_next(true);
+    pp_barrier();
+    mfma_q(1, 0);
+    if (more && wm == 0) wait_next(true);
+    pp_barrier();
+  }
+  if (wm == 0) pp_barrier();   // realign the two wave rows
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue (as conv_nt_v2_kernel): flat fragment view fi' = qm*4 + fi, fj' = qn*2 + fj
+  constexpr int FM = 8, FN = 4, WMW = 2, WM = 128;
+  auto A_ = [&](int fi, int fj) -> f32x4_t& { return acc[fi >> 2][fj >> 1][fi & 3][fj & 1]; };
+  auto row_of = [&](int fi, int k) { return (fi >> 2) * 128 + wm * 64 + (fi & 3) * 16 + lq * 4 + k; };
+  auto col_of = [&](int fj) { return (fj >> 1) * 128 + wn * 32 + (fj & 1) * 16 + lr; };
+  const bool col_writer = lq == 0;
+  const int rows_valid = (int)((M - m0) < BM ? (M - m0) : BM);
+  float* red = (float*)smem;
+  if (a.stats && rows_valid == BM) {
+    float2* red2 = (float2*)smem;
+    constexpr float NL = (float)(4 * FM);
+    float sj[FN], mj[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float x = A_(i, j)[k];
+          sm += x;
+          sq = __builtin_fmaf(x, x, sq);
+        }
+      sj[j] = sm;
+      mj[j] = fmaxf(sq - sm * sm * (1.f / NL), 0.f);
+    }
+    float n = NL;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
+        const float d = (s2 - sj[j]) / n;
+        mj[j] = mj[j] + m2 + d * d * (0.5f * n);
+        sj[j] += s2;
+      }
+      n *= 2.f;
+    }
+    if (col_writer)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
+    __syncthreads();
+    if (wm == 0 && col_writer) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = col_of(j);
+        float2 t = red2[c];
+        float ntot = (float)WM;
+#pragma unroll
+        for (int w = 1; w < WMW; ++w) {
+          const float2 u = red2[w * BN + c];
+          const float d = u.x / (float)WM - t.x / ntot;
+          t.y = t.y + u.y + d * d * (ntot * (float)WM / (ntot + (float)WM));
+          t.x += u.x;
+          ntot += (float)WM;
+        }
+        if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = t;
+      }
+    }
+    __syncthreads();
+  } else if (a.stats) {
+    float cs[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += row_of(i, k) < rows_valid ? A_(i, j)[k] : 0.f;
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
+      cs[j] = v;
+    }
+    if (col_writer)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
+    __syncthreads();
+    float mean[FN], tot[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = col_of(j);
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
+      tot[j] = t;
+      mean[j] = t / (float)rows_valid;
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d = A_(i, j)[k] - mean[j];
+          v += row_of(i, k) < rows_valid ? d * d : 0.f;
+        }
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
+      cs[j] = v;
+    }
+    __syncthreads();
+    if (col_writer)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
+    __syncthreads();
+    if (wm == 0 && col_writer) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = col_of(j);
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
+        if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = make_float2(tot[j], t);
+      }
+    }
+    __syncthreads();
+  }
+  float* stage = (float*)smem;
+  bf16_t* Y = (bf16_t*)a.y;
+  const bf16_t* R1 = (const bf16_t*)a.r;
+  const bf16_t* R2 = (const bf16_t*)a.r2;
+  const int s_rl = tid >> 3, s_cc = tid & 7;
+#pragma unroll
+  for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
+    const int cbase = pass * EPI_COLS;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = col_of(j);
+      if (col >= cbase && col < cbase + EPI_COLS) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = A_(i, j)[k];
+      }
+    }
+    __syncthreads();
+    const int n = n0 + cbase + s_cc * 8;
+    if (n < a.Co) {
+#pragma unroll
+      for (int rr = 0; rr < BM / 64; ++rr) {
+        const int row = s_rl + 64 * rr;
+        const long m = m0 + row;
+        if (m < M) {
+          const float* sp = stage + row * EPI_LD + s_cc * 8;
+          const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
+          float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          if (R1) {
+            float u[8];
+            Vec8<bf16_t>::load(R1 + (size_t)m * a.ldr + n, u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += u[e];
+          }
+          if (R2) {
+            float u[8];
+            Vec8<bf16_t>::load(R2 + (size_t)m * a.ldr2 + n, u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += u[e];
+          }
+          Vec8<bf16_t>::store(Y + (size_t)m * a.ldy + n, v);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// (the body is a device function: the host pass does not parse buffer-resource values)
+template <int ST>
+__global__ __launch_bounds__(PP_THREADS, 1) void conv_nt_pp_kernel(ConvArgs a) {
+  conv_nt_pp_body<ST>(a);
+}
+
+template <int ST>
+hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
+  static_assert(256 * EPI_LD * 4 <= PP_LDS, "epilogue staging fits the ring");
+  auto kern = conv_nt_pp_kernel<ST>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const long M = (long)a.N * a.Ho * a.Wo;
+  const int nwg = ceil_div(M, 256) * ceil_div(a.Co, 256);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(PP_THREADS), PP_LDS, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// ping-pong config: the v2 fast-path preconditions (conv_nt_v2_ok, no tap8), Co > 128 and an
+// operands of < 2^31 bytes (32-bit buffer offsets), kernels up to 4 x 4 (tap validity bits)
+bool conv_nt_pp_ok(const ConvArgs& a) {
+  return !a.tap8 && a.Co > 128 && a.KH <= 4 && a.KW <= 4 && conv_nt_v2_ok(a) &&
+         (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31) && (long)a.Co * a.ldw * 2 < (1L << 31);
+}
+
+hipError_t launch_conv_nt_pp(const ConvArgs& a, hipStream_t s) {
+  if (a.st == 1) return pp_launch<1>(a, s);
+  if (a.st == 2) return pp_launch<2>(a, s);
+  return hipErrorInvalidValue;
+}

@@ -15,6 +15,7 @@
 //    mean) for the fused batch-norm.
 #include "conv.h"
 #include <algorithm>
+#include <cstdlib>
 
 #ifndef SEG_MFMA_PRIO
 #define SEG_MFMA_PRIO 1   // s_setprio(1) around MFMA clusters (+1-2 % measured)
@@ -129,10 +130,13 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
     a_w0[i] = wo * a.sf - a.pad_w;
   }
 
+  // K-step order (not tap8): channel chunk outer, tap inner -- the KH*KW shifted reads of one
+  // chunk's source rows follow each other while they are still in L2
+  const int ntaps = a.KH * a.KW;
+  auto kcol = [&](int kb) { return T8 ? kb * BK : (kb % ntaps) * a.C + (kb / ntaps) * BK; };
   auto issue_a = [&](int kb, int stage) {
-    const int k0 = kb * BK;
-    const int tap = k0 / a.C;
-    const int c0 = T8 ? 0 : k0 - tap * a.C;
+    const int tap = T8 ? 0 : kb % ntaps;
+    const int c0 = T8 ? 0 : (kb / ntaps) * BK;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     const int dh = kh * a.dil, dw = kw * a.dil;
     char* sA = smem + stage * STAGE_BYTES;
@@ -160,7 +164,7 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
     }
   };
   auto issue_b = [&](int kb, int stage) {
-    const int k0 = kb * BK;
+    const int k0 = kcol(kb);
     char* sB = smem + stage * STAGE_BYTES + BM * 128;
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
@@ -438,6 +442,16 @@ hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
 
 }  // namespace
 
+// SEG_NT_PP=0 selects the v2 main loop for Co > 128 (A/B switch); default: ping-pong
+bool conv_nt_pp_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("SEG_NT_PP");
+    on = e && e[0] == '0' ? 0 : 1;
+  }
+  return on != 0;
+}
+
 // bf16 fast path: C % 64 == 0, ld/co multiples of 8; stats tiles are 256 rows
 bool conv_nt_v2_ok(const ConvArgs& a) {
   if (a.tap8)   // padded stem: 8-channel taps, weights [Co][ldw >= ceil(KH*KW*8/64)*64]
@@ -457,7 +471,10 @@ int conv_nt_v2_rows(const ConvArgs& a) {
 
 template <int ST>
 hipError_t v2_dispatch(const ConvArgs& a, hipStream_t s) {
-  if (a.Co > 128) return v2_launch<256, 4, 2, 2, ST>(a, s);
+  if (a.Co > 128) {
+    if (conv_nt_pp_enabled() && conv_nt_pp_ok(a)) return launch_conv_nt_pp(a, s);
+    return v2_launch<256, 4, 2, 2, ST>(a, s);
+  }
   if (a.Co > 64) return v2_launch<128, 4, 2, 3, ST>(a, s);
   return v2_launch<64, 8, 1, 3, ST>(a, s);
 }
