@@ -29,8 +29,10 @@ sys.path[:0] = [REPO, PKG]
 H, W, NB = 1024, 2048, 4
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_TBS = 8.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 CLS_NAMES = {0: "conv_nt_kernel (forward implicit GEMM)", 1: "conv_nt_kernel (data-gradient)",
-             2: "conv_wgrad_kernel (weight-gradient, split-K)"}
+             2: "conv_wgrad_kernel (weight-gradient, split-K)", 3: "bn_apply (BN + ReLU + residual)",
+             4: "bn_bwd_reduce", 5: "bn_bwd_apply"}
 
 
 def cpu_baseline(threads, pyramid):
@@ -102,13 +104,15 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    if not args.no_profile:
-        ctx.profile(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    # HIP-event kernel timing (roofline) is recorded on the launch stream during the LAST timed
+    # step only: events around every conv launch of every step cost ~1.8 ms per step
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if i == args.steps - 1 and not args.no_profile:
+            ctx.profile(True)
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -126,6 +130,20 @@ def main():
     roofline = None
     if not args.no_profile:
         cls = {c: ctx.profile_read(c) for c in (0, 1, 2)}
+        # every profiled class against its own roofline: conv classes in TFLOP/s vs the bf16
+        # MFMA peak, BN streaming classes in TB/s of algorithmic bytes vs HBM peak
+        bn = {c: ctx.profile_read(c) for c in (3, 4, 5)}
+        all_classes = {}
+        for c, r_ in list(cls.items()) + list(bn.items()):
+            if r_["ms"] <= 0:
+                continue
+            conv = c < 3
+            ach = r_["gflop"] / r_["ms"]   # GFLOP/ms = TFLOP/s; GB/ms = TB/s
+            pk = (PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS) if conv else PEAK_HBM_TBS
+            all_classes[CLS_NAMES[c]] = {"ms": round(r_["ms"], 3), "launches": r_["launches"],
+                                         "achieved": round(ach, 2),
+                                         "unit": "TFLOP/s" if conv else "TB/s",
+                                         "peak": pk, "frac": round(ach / pk, 4)}
         dom = max(cls, key=lambda c: cls[c]["ms"])
         r = cls[dom]
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
@@ -146,9 +164,10 @@ def main():
                     "kernel": CLS_NAMES[dom],
                     "launches": r["launches"],
                     "avg_launch_ms": round(r["ms"] / max(r["launches"], 1), 4),
-                    "share_of_step": round(r["ms"] / (elapsed * 1e3), 3),
-                    "classes_ms_per_step": {CLS_NAMES[c]: round(cls[c]["ms"] / args.steps, 2)
-                                            for c in cls},
+                    "share_of_step": round(r["ms"] / (elapsed * 1e3 / args.steps), 3),
+                    "profiled_steps": 1,
+                    "classes_ms_per_step": {CLS_NAMES[c]: round(cls[c]["ms"], 2) for c in cls},
+                    "classes": all_classes,
                     "max_layer": r["max_layer"]}
         ctx.profile(False)
 

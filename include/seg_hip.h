@@ -127,6 +127,12 @@ int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, 
                       const void* x, int H, int W, int Ci, int ldx, int k, int stride, int rate,
                       int explicit_pad, float* dw, void* workspace, int64_t ws_bytes,
                       void* stream);
+/* bf16 weight gradient with an explicit tile (bm co x bn columns, each 64/128/256) and
+ * split count: reaches every kernel configuration at test sizes (256 x 256 = ping-pong) */
+int seg_op_conv_wgrad_cfg(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
+                          const void* x, int H, int W, int Ci, int ldx, int k, int stride, int rate,
+                          int explicit_pad, float* dw, void* workspace, int64_t ws_bytes, int bm,
+                          int bn, int splits, void* stream);
 
 #ifdef __cplusplus
 }

@@ -64,8 +64,12 @@ hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s);
 bool conv_nt_pp_ok(const ConvArgs& a);
 bool conv_nt_pp_enabled();
 hipError_t launch_conv_nt_pp(const ConvArgs& a, hipStream_t s);
+// ping-pong 256x256 weight gradient (conv_pp.hip), used when the v2 tile choice is 256 x 256
+bool conv_wgrad_pp_ok(const WgradArgs& a);
+hipError_t launch_conv_wgrad_pp(const WgradArgs& a, hipStream_t s);
 bool conv_wgrad_v2_ok(const WgradArgs& a);
 hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s);
+hipError_t launch_conv_wgrad_v2_tile(const WgradArgs& a, int bm, int bn, hipStream_t s);
 void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn);
 
 // 3-channel stem in bf16, laid out as 8-channel taps (tap8 mode):

@@ -459,3 +459,299 @@ hipError_t launch_conv_nt_pp(const ConvArgs& a, hipStream_t s) {
   if (a.st == 2) return pp_launch<2>(a, s);
   return hipErrorInvalidValue;
 }
+
+// ======================================================================================
+// bf16 weight gradient, ping-pong schedule: C[co][tap*Ci+ci] = sum_p dy[p][co] * x[src(p,tap)][ci]
+//
+// The NT kernel's main loop transposed to the TN problem of conv_wgrad_v2_kernel: 256 (co) x
+// 256 (tap,ci) tile, 8 waves as 2 x 4 with 128 x 64 wave tiles in four 64 x 32 quadrants; a
+// K-tile is 64 pixels; each half-tile is 64 pixel rows x 256 B (128 co of dy, or 128 columns
+// of the gathered x) read by ds_read_b64_tr_b16 through the XOR swizzle of the v2 kernel.
+// Operands come through buffer resources: dy rows are one add per DMA, x rows are decoded once
+// per K-tile and lane (pixel -> n, ho, wo by row carries) and shared by both x halves.
+// Split-K over pixels into fp32 slabs as in v2 (reduced by splitk_reduce).
+// ======================================================================================
+namespace {
+
+constexpr int WHALF = 64 * 256;
+constexpr int WBUF = 4 * WHALF;
+constexpr int WPP_LDS = 2 * WBUF;
+
+__device__ __forceinline__ int wpp_swz(int row, int ch) { return ch ^ (2 * (row & 3) + 8 * ((row >> 3) & 1)); }
+
+template <int FAST>   // FAST: Wo >= 64 (a K-tile's rows need at most one row carry)
+__device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
+  constexpr int BM = 256, BN = 256, PK = 64;
+  constexpr uint32_t OOB = 0x80000000u;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int Ncol = a.KH * a.KW * a.C;
+  const int P = a.N * a.Ho * a.Wo;
+  const int mtn = (a.Co + BM - 1) / BM, ntn = (Ncol + BN - 1) / BN;
+  const int nwg = mtn * ntn * a.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = wg / (mtn * ntn);
+  const int rem = wg - split * mtn * ntn;
+  const int nt_ = rem / mtn, mt_ = rem - nt_ * mtn;
+  const int m0 = mt_ * BM, n0 = nt_ * BN;
+  const int chunk = ((P + a.splits - 1) / a.splits + PK - 1) / PK * PK;
+  const int p_begin = split * chunk;
+  const int p_end = (p_begin + chunk < P) ? p_begin + chunk : P;
+  const int nk = p_end > p_begin ? (p_end - p_begin + PK - 1) / PK : 0;
+
+  const auto rs_dy = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, (int)((long)P * a.lddy * 2), 0x00020000);
+  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0,
+                                                      (int)((long)a.N * a.H * a.W * a.ldx * 2), 0x00020000);
+
+  // DMA rows: instruction i -> pixel row r_i = (i*8 + wave)*4 + lane/16, physical chunk lane&15
+  const int pc = lane & 15;
+  int r_[2];
+  uint32_t a_voff[4];          // j = half*2 + i: dy byte offset of (row r_i, co) (OOB: co >= Co)
+  int b_dh[4], b_dw[4], b_toff[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) r_[i] = (i * 8 + wave) * 4 + (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = j & 1, h = j >> 1;
+    const int lc = wpp_swz(r_[i], pc);
+    const int co = m0 + h * 128 + lc * 8;
+    a_voff[j] = co < a.Co ? (uint32_t)((r_[i] * a.lddy + co) * 2) : OOB;
+    const int col = n0 + h * 128 + lc * 8;
+    const bool okc = col < Ncol;
+    const int cc = okc ? col : 0;
+    const int tap = cc / a.C, ci = cc - tap * a.C;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    b_dh[j] = okc ? kh * a.dil - a.pad_h : -(1 << 28);
+    b_dw[j] = kw * a.dil - a.pad_w;
+    b_toff[j] = (b_dh[j] * a.W + b_dw[j]) * a.ldx + ci;
+  }
+
+  // next K-tile to issue: first pixel p0 decoded to (n, ho, wo), stepped by PK pixels
+  int nx_p0 = p_begin, nx_n, nx_ho, nx_wo;
+  {
+    nx_wo = p_begin % a.Wo;
+    const int t = p_begin / a.Wo;
+    nx_ho = t % a.Ho;
+    nx_n = t / a.Ho;
+  }
+  // per-lane x-row decode of the K-tile being issued (shared by both x halves)
+  int hb[2], wb[2], pixb[2];
+  bool pv[2];
+  int cur_p0 = 0, cur_prem = 0;
+  auto decode_next = [&]() {
+    cur_p0 = nx_p0;
+    cur_prem = p_end - nx_p0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int n, ho, wo;
+      if constexpr (FAST) {
+        wo = nx_wo + r_[i];
+        const bool c = wo >= a.Wo;
+        wo = c ? wo - a.Wo : wo;
+        ho = nx_ho + (c ? 1 : 0);
+        const bool c2 = ho == a.Ho;
+        ho = c2 ? 0 : ho;
+        n = nx_n + (c2 ? 1 : 0);
+      } else {
+        const int p = nx_p0 + r_[i];
+        wo = p % a.Wo;
+        const int t = p / a.Wo;
+        ho = t % a.Ho;
+        n = t / a.Ho;
+      }
+      hb[i] = ho * a.sf;
+      wb[i] = wo * a.sf;
+      pixb[i] = ((n * a.H + hb[i]) * a.W + wb[i]) * a.ldx;
+      pv[i] = r_[i] < cur_prem;
+    }
+    nx_p0 += PK;
+    nx_wo += PK;
+    while (nx_wo >= a.Wo) {
+      nx_wo -= a.Wo;
+      if (++nx_ho == a.Ho) { nx_ho = 0; ++nx_n; }
+    }
+  };
+
+  // half ids: 0 = dy co 0-127, 1 = dy co 128-255, 2 = x cols 0-127, 3 = x cols 128-255
+  auto issue_half = [&](int kb, int hid) {
+    char* dst = smem + (kb & 1) * WBUF + hid * WHALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      auto* ldst = (__attribute__((address_space(3))) void*)(dst + (i * 8 + wave) * 1024);
+      if (hid < 2) {
+        const int j = hid * 2 + i;
+        const uint32_t off = r_[i] < cur_prem ? a_voff[j] + (uint32_t)(cur_p0 * a.lddy * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_dy, ldst, 16, off, 0, 0, 0);
+      } else {
+        const int j = (hid - 2) * 2 + i;
+        const int hi = hb[i] + b_dh[j], wi = wb[i] + b_dw[j];
+        const bool ok = pv[i] & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
+        const uint32_t off = ok ? (uint32_t)((pixb[i] + b_toff[j]) * 2) : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, ldst, 16, off, 0, 0, 0);
+      }
+    }
+  };
+
+  f32x4_t acc[2][2][4][2];
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // transposed fragment reads (ds_read_b64_tr_b16) as inline asm: with the compiler's own
+  // intrinsic hipcc waits vmcnt(0) before every read (it cannot prove that the LDS-DMA in
+  // flight does not alias it), which drains the prefetch each phase. The reads are ordered
+  // by the barrier protocol above; the MFMA segment waits lgkmcnt(0) before using them.
+  // Fragment f of a quadrant: LDS byte address base + k-substep s * 32 rows (+8192) and the
+  // second 4-row group (+1024); the per-lane base (row kr = 8*lq + q4, swizzled column
+  // chunk) is loop-invariant.
+  const int lq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const uint32_t smem_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto tr_base = [&](int col) -> uint32_t {
+    const int kr = 8 * lq + q4;
+    return (uint32_t)(kr * 256 + wpp_swz(kr, col >> 3) * 16 + (col & 7) * 2);
+  };
+  uint32_t a_rb[4], b_rb[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a_rb[i] = tr_base(wm * 64 + i * 16 + 4 * p4);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b_rb[j] = tr_base(wn * 32 + j * 16 + 4 * p4);
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  auto frag2 = [&](uint32_t addr, bf16x8_t& f0, bf16x8_t& f1) {   // k-substeps 0 and 1
+    s16x4_t l0, h0, l1, h1;
+    asm volatile("ds_read_b64_tr_b16 %0, %4\n\t"
+                 "ds_read_b64_tr_b16 %1, %4 offset:1024\n\t"
+                 "ds_read_b64_tr_b16 %2, %4 offset:8192\n\t"
+                 "ds_read_b64_tr_b16 %3, %4 offset:9216"
+                 : "=&v"(l0), "=&v"(h0), "=&v"(l1), "=&v"(h1) : "v"(addr));
+    const s16x8_t v0 = __builtin_shufflevector(l0, h0, 0, 1, 2, 3, 4, 5, 6, 7);
+    const s16x8_t v1 = __builtin_shufflevector(l1, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+    __builtin_memcpy(&f0, &v0, 16);
+    __builtin_memcpy(&f1, &v1, 16);
+  };
+  bf16x8_t af[4][2], bfr[2][2];
+  auto read_a = [&](int kb, int qm) {
+    const uint32_t off = smem_lds + (kb & 1) * WBUF + qm * WHALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) frag2(off + a_rb[i], af[i][0], af[i][1]);
+  };
+  auto read_b = [&](int kb, int qn) {
+    const uint32_t off = smem_lds + (kb & 1) * WBUF + (2 + qn) * WHALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) frag2(off + b_rb[j], bfr[j][0], bfr[j][1]);
+  };
+  auto mfma_q = [&](int qm, int qn) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm fragment reads
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[qm][qn][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto wait_next = [&](bool more) {
+    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  if (nk > 0) {
+    decode_next();
+    issue_half(0, 0);
+    issue_half(0, 2);
+    issue_half(0, 3);
+    issue_half(0, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    pp_barrier();
+    if (wm == 1) pp_barrier();
+    for (int kb = 0; kb < nk; ++kb) {
+      const bool more = kb + 1 < nk;
+      if (more) decode_next();   // K-tile kb + 1
+      read_a(kb, 0);
+      read_b(kb, 0);
+      if (more) issue_half(kb + 1, 0);
+      if (wm == 1) wait_next(more);
+      pp_barrier();
+      mfma_q(0, 0);
+      if (wm == 0) wait_next(more);
+      pp_barrier();
+      read_b(kb, 1);
+      if (more) issue_half(kb + 1, 2);
+      if (wm == 1) wait_next(more);
+      pp_barrier();
+      mfma_q(0, 1);
+      if (wm == 0) wait_next(more);
+      pp_barrier();
+      read_a(kb, 1);
+      if (more) issue_half(kb + 1, 3);
+      pp_barrier();
+      mfma_q(1, 1);
+      pp_barrier();
+      read_b(kb, 0);
+      if (more) issue_half(kb + 1, 1);
+      if (more && wm == 1) wait_next(true);
+      pp_barrier();
+      mfma_q(1, 0);
+      if (more && wm == 0) wait_next(true);
+      pp_barrier();
+    }
+    if (wm == 0) pp_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+
+  float* O = a.out + (size_t)split * a.Co * Ncol;
+  const int lr = lane & 15;
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = n0 + qn * 128 + wn * 32 + j * 16 + lr;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + qm * 128 + wm * 64 + i * 16 + lq * 4 + r;
+            if (m < a.Co && n < Ncol) O[(size_t)m * Ncol + n] = acc[qm][qn][i][j][r];
+          }
+        }
+}
+
+template <int FAST>
+__global__ __launch_bounds__(PP_THREADS, 1) void conv_wgrad_pp_kernel(WgradArgs a) {
+  conv_wgrad_pp_body<FAST>(a);
+}
+
+}  // namespace
+
+// 256 x 256 wgrad tiles with operands < 2^31 bytes (32-bit buffer offsets)
+bool conv_wgrad_pp_ok(const WgradArgs& a) {
+  const long P = (long)a.N * a.Ho * a.Wo;
+  return (a.C % 8) == 0 && (a.ldx % 8) == 0 && (a.Co % 8) == 0 && (a.lddy % 8) == 0 &&
+         P * a.lddy * 2 < (1L << 31) && (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31);
+}
+
+hipError_t launch_conv_wgrad_pp(const WgradArgs& a, hipStream_t s) {
+  const int Ncol = a.KH * a.KW * a.C;
+  const int nwg = ceil_div(a.Co, 256) * ceil_div(Ncol, 256) * a.splits;
+  auto launch = [&](auto kern) -> hipError_t {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WPP_LDS);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(PP_THREADS), WPP_LDS, s, a);
+    return hipGetLastError();
+  };
+  if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<1>);
+  return launch(conv_wgrad_pp_kernel<0>);
+}

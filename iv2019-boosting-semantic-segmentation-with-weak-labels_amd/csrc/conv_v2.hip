@@ -740,6 +740,11 @@ void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn) {
 hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s) {
   int bm, bn;
   conv_wgrad_v2_tile(a.Co, a.KH * a.KW * a.C, (long)a.N * a.Ho * a.Wo, &bm, &bn);
+  return launch_conv_wgrad_v2_tile(a, bm, bn, s);
+}
+
+// explicit tile (bm, bn in {64, 128, 256}); 256 x 256 runs the ping-pong kernel
+hipError_t launch_conv_wgrad_v2_tile(const WgradArgs& a, int bm, int bn, hipStream_t s) {
   if (bm == 64) {
     if (bn == 64) return wg2_launch<64, 64, 4, 2, 3>(a, s);
     if (bn == 128) return wg2_launch<64, 128, 2, 4, 3>(a, s);
@@ -752,5 +757,6 @@ hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s) {
   }
   if (bn == 64) return wg2_launch<256, 64, 8, 1, 3>(a, s);
   if (bn == 128) return wg2_launch<256, 128, 4, 2, 3>(a, s);
+  if (conv_nt_pp_enabled() && conv_wgrad_pp_ok(a)) return launch_conv_wgrad_pp(a, s);
   return wg2_launch<256, 256, 2, 4, 2>(a, s);
 }

@@ -1333,4 +1333,28 @@ int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, 
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_wgrad");
 }
 
+int seg_op_conv_wgrad_cfg(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
+                          const void* x, int H, int W, int Ci, int ldx, int k, int stride, int rate,
+                          int explicit_pad, float* dw, void* workspace, int64_t ws_bytes, int bm,
+                          int bn, int splits, void* stream) {
+  if (dtype != SEG_DTYPE_BF16) return set_err(nullptr, -EINVAL, "wgrad_cfg: bf16 only");
+  if ((bm != 64 && bm != 128 && bm != 256) || (bn != 64 && bn != 128 && bn != 256) || splits < 1)
+    return set_err(nullptr, -EINVAL, "wgrad_cfg: tile must be 64/128/256, splits >= 1");
+  int ho, wo, ph, pw;
+  op_geom(H, W, k, stride, rate, explicit_pad, &ho, &wo, &ph, &pw);
+  if (ho != Ho || wo != Wo) return set_err(nullptr, -EINVAL, "wgrad geometry mismatch");
+  WgradArgs a{};
+  a.dy = dy; a.lddy = lddy; a.x = x; a.N = N; a.H = H; a.W = W; a.C = Ci; a.ldx = ldx;
+  a.Ho = Ho; a.Wo = Wo; a.Co = Co; a.KH = a.KW = k; a.sf = stride; a.pad_h = ph; a.pad_w = pw;
+  a.dil = rate; a.splits = splits;
+  const long n = (long)Co * k * k * Ci;
+  if ((int64_t)splits * n * 4 > ws_bytes) return set_err(nullptr, -EINVAL, "wgrad_cfg: workspace");
+  if (!conv_wgrad_v2_ok(a)) return set_err(nullptr, -EINVAL, "wgrad_cfg: shape not on the v2 path");
+  a.out = (float*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = launch_conv_wgrad_v2_tile(a, bm, bn, s);
+  if (e == hipSuccess) e = launch_splitk_reduce((float*)workspace, splits, n, n, dw, 0, s);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_wgrad_cfg");
+}
+
 }  // extern "C"

@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = [
     "seg_backward", "seg_apply_update", "seg_outputs", "seg_confusion", "seg_debug_tensor",
     "seg_profile", "seg_profile_dump",
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
-    "seg_op_conv_wgrad",
+    "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg",
 ]
 
 PYRAMID = {"none": 0, "psp": 1, "aspp": 2}
@@ -85,6 +85,8 @@ def _load():
                                    ip, vp]),
         "seg_op_conv_wgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, ip,
                                    vp, vp, i64, vp]),
+        "seg_op_conv_wgrad_cfg": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip,
+                                       ip, vp, vp, i64, ip, ip, ip, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

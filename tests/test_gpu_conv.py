@@ -149,3 +149,41 @@ def test_conv_wgrad(cuda, dtype, case):
     torch.cuda.synchronize()
     tol = 1e-4 if dtype == "fp32" else 2e-2
     assert _rel(dw.cpu().numpy(), ref) < tol
+
+
+WGRAD_CFG_CASES = [
+    # case (N, H, W, Ci, Co, k, stride, rate, explicit_pad), bm, bn, splits
+    ((1, 8, 72, 256, 256, 3, 1, 2, False), 256, 256, 3),   # ping-pong, Wo >= 64 (row carries)
+    ((2, 13, 17, 128, 256, 3, 1, 2, False), 256, 256, 2),  # ping-pong, Wo < 64, ragged columns
+    ((1, 9, 70, 64, 320, 1, 1, 1, False), 256, 256, 4),    # ragged co tile, Ncol < 256
+    ((2, 18, 132, 64, 256, 3, 2, 1, True), 256, 256, 5),   # stride-2 conv2d_same gather
+    ((1, 6, 66, 256, 256, 3, 1, 4, False), 256, 256, 64),  # splits with no pixels (zero slabs)
+    ((2, 13, 17, 128, 256, 3, 1, 2, False), 128, 256, 3),  # v2 configurations
+    ((1, 8, 72, 256, 256, 1, 1, 1, False), 64, 128, 2),
+]
+
+
+@pytest.mark.parametrize("case,bm,bn,splits", WGRAD_CFG_CASES)
+def test_conv_wgrad_cfg(cuda, case, bm, bn, splits):
+    """bf16 weight gradient at an explicit tile / split configuration (every kernel the
+    runtime can pick, reached at test sizes), vs float64 on the same bf16 operands."""
+    from seg_hip import LIB, check
+    N, H, W, Ci, Co, k, s, r, ep = case
+    x, w = _tensors(case)
+    spec, Ho, Wo = _geom(case)
+    g = _bf16_round(np.random.default_rng(3).standard_normal((N, Ho, Wo, Co)).astype(np.float32))
+    x = _bf16_round(x)
+    wt = torch.as_tensor(w, dtype=torch.float64).requires_grad_(True)
+    y = conv_tf(torch.as_tensor(x, dtype=torch.float64).permute(0, 3, 1, 2), wt, spec)
+    y.backward(torch.as_tensor(g, dtype=torch.float64).permute(0, 3, 1, 2))
+    ref = wt.grad.numpy()
+    xd = torch.as_tensor(x).to(cuda, torch.bfloat16).contiguous()
+    gd = torch.as_tensor(g).to(cuda, torch.bfloat16).contiguous()
+    dw = torch.zeros((Co, k, k, Ci), dtype=torch.float32, device=cuda)
+    ws = torch.full((splits * Co * k * k * Ci,), float("nan"), dtype=torch.float32, device=cuda)
+    check(LIB.seg_op_conv_wgrad_cfg(1, gd.data_ptr(), N, Ho, Wo, Co, Co, xd.data_ptr(), H, W, Ci,
+                                    Ci, k, s, r, int(ep), dw.data_ptr(), ws.data_ptr(),
+                                    ws.numel() * 4, bm, bn, splits,
+                                    torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert _rel(dw.cpu().numpy(), ref) < 2e-2
