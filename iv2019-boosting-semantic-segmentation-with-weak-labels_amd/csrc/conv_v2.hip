@@ -618,8 +618,19 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   auto tr_read = [&](const char* base, int rowb, int row, int col) -> s16x4_t {
     const int lc = col >> 3, within = (col & 7) * 2;
     const int ph = rowb >= 256 ? lc ^ (2 * (row & 3) + 8 * ((row >> 3) & 1)) : lc ^ (2 * (row & 3));
+#ifdef WG2_TR_BUILTIN
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (s16x4_t __attribute__((address_space(3)))*)(base + row * rowb + ph * 16 + within));
+#else
+    // inline asm: the builtin makes hipcc wait vmcnt(0) (every LDS-DMA in flight) before the
+    // read, which defeats the STAGES-deep ring; ordering is by the counted vmcnt + barrier, and
+    // compute() waits lgkmcnt(0) before the MFMAs
+    const uint32_t addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)(
+        base + row * rowb + ph * 16 + within);
+    s16x4_t r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+    return r;
+#endif
   };
 
   auto compute = [&](int stg) {
@@ -643,6 +654,10 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
         short t8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         __builtin_memcpy(&bfr[j], t8, 16);
       }
+#ifndef WG2_TR_BUILTIN
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #if SEG_MFMA_PRIO
       __builtin_amdgcn_s_setprio(1);
 #endif

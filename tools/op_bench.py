@@ -15,6 +15,10 @@ SHAPES = {  # N, H, W, Ci, Co, k, stride, rate
     "b3c1": (4, 128, 256, 1024, 256, 1, 1, 1),
     "b3c3": (4, 128, 256, 256, 1024, 1, 1, 1),
     "head1": (4, 128, 256, 256, 256, 1, 1, 1),
+    "b1c2": (4, 256, 512, 64, 64, 3, 1, 1),
+    "b1c3": (4, 256, 512, 64, 256, 1, 1, 1),
+    "b2c2": (4, 128, 256, 128, 128, 3, 1, 1),
+    "b2c1": (4, 128, 256, 512, 128, 1, 1, 1),
 }
 op = sys.argv[1] if len(sys.argv) > 1 else "wgrad"
 N, H, W, Ci, Co, k, s, r = SHAPES[sys.argv[2] if len(sys.argv) > 2 else "b4c2"]
