@@ -100,6 +100,18 @@ int seg_outputs(seg_ctx* ctx, const float** losses, const float** reg,
 int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions, int64_t n,
                   int num_classes, int32_t* cm, void* stream);
 
+/* weak-label maps on the device (input_subset_bboxes_v2.py:74-98 rasterisation fused with the
+ * aspect-preserving nearest-neighbour resize + crop of input_pipelines/utils.py:181-241;
+ * input_subset_image_labels.py:73-107 for tags). All pointers are device memory:
+ *   boxes [total][4] (xmin, xmax, ymin, ymax) normalised to [0,1], cids [total] in [0,13],
+ *   box_off [n+1] per-image prefix offsets into boxes, geom [n][6] = (src_h, src_w, resized_h,
+ *   resized_w, crop_y, crop_x); max_boxes = the largest per-image count (<= 1024);
+ *   out [n][H][W][15] fp32 multinomials (channel 14 = void). tags [n][15] normalised. */
+int seg_bbox_labels(const float* boxes, const int32_t* cids, const int32_t* box_off,
+                    const int32_t* geom, int n, int max_boxes, int H, int W, float* out,
+                    void* stream);
+int seg_tag_labels(const float* tags, int n, int H, int W, float* out, void* stream);
+
 /* internal tensors for parity tests: "logits", "grad_un", "dzscale", "feat", "dfeat",
  * "head<h>_out", "head<h>_dout", "conv<i>_x" (input of the last forward), "conv<i>_y",
  * "conv<i>_dy" (i = creation index).

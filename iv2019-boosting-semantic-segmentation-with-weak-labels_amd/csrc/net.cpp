@@ -16,6 +16,7 @@
 #include "bn.h"
 #include "conv.h"
 #include "loss.h"
+#include "labels.h"
 #include "optim.h"
 #include "pool.h"
 
@@ -1177,6 +1178,26 @@ int seg_confusion(seg_ctx* c, const int32_t* labels, const int32_t* decisions, i
   if (e == hipSuccess) e = launch_confusion(labels, decisions, n, num_classes, cm, s);
   if (e != hipSuccess) return hip_fail(c, e, "seg_confusion");
   return 0;
+}
+
+int seg_bbox_labels(const float* boxes, const int32_t* cids, const int32_t* box_off,
+                    const int32_t* geom, int n, int max_boxes, int H, int W, float* out,
+                    void* stream) {
+  if (n < 0 || H <= 0 || W <= 0 || (n > 0 && (!box_off || !geom || !out)))
+    return set_err(nullptr, -EINVAL, "seg_bbox_labels: bad arguments");
+  if (max_boxes < 0 || max_boxes > 1024)
+    return set_err(nullptr, -E2BIG, "seg_bbox_labels: at most 1024 boxes per image (reference 516)");
+  static_assert(sizeof(BboxGeom) == 6 * sizeof(int32_t), "geom layout");
+  hipError_t e = launch_bbox_labels(boxes, cids, box_off, (const BboxGeom*)geom, n, H, W, out,
+                                    (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_bbox_labels");
+}
+
+int seg_tag_labels(const float* tags, int n, int H, int W, float* out, void* stream) {
+  if (n < 0 || H <= 0 || W <= 0 || (n > 0 && (!tags || !out)))
+    return set_err(nullptr, -EINVAL, "seg_tag_labels: bad arguments");
+  hipError_t e = launch_tag_labels(tags, n, H, W, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_tag_labels");
 }
 
 int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* ld, int* dtype) {

@@ -11,6 +11,13 @@ produced by the fused update (it needs the weights of this step, read once there
 is valid after the step's train_op has run.
 """
 from estimator.mode_keys import ModeKeys
+from input_pipelines.weak_labels import BboxLabelsGPU, BoxLists, TagSets
+
+
+def _weak_maps(ctx):
+    if getattr(ctx, '_weak_maps', None) is None:
+        ctx._weak_maps = BboxLabelsGPU(ctx.cfg.height, ctx.cfg.width, ctx.device)
+    return ctx._weak_maps
 
 
 class Losses(dict):
@@ -44,6 +51,11 @@ def define_losses(mode, predictions, labels, config, params):  # pylint: disable
     px = labels.get('prolabels_per_pixel')
     bb = labels.get('prolabels_per_bbox')
     tg = labels.get('prolabels_per_image')
+    # weak labels given as box lists / tag sets are rasterised on the device (labels.hip)
+    if isinstance(bb, BoxLists):
+        bb = _weak_maps(ctx).bbox(bb) if len(bb) else None
+    if isinstance(tg, TagSets):
+        tg = _weak_maps(ctx).tags(tg) if len(tg) else None
     ctx.loss(px if px is not None and px.numel() else None,
              bb if bb is not None and bb.numel() else None,
              tg if tg is not None and tg.numel() else None,

@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = [
     "seg_backward", "seg_apply_update", "seg_outputs", "seg_confusion", "seg_debug_tensor",
     "seg_profile", "seg_profile_dump",
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
-    "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg",
+    "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
 ]
 
 PYRAMID = {"none": 0, "psp": 1, "aspp": 2}
@@ -87,6 +87,8 @@ def _load():
                                    vp, vp, i64, vp]),
         "seg_op_conv_wgrad_cfg": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip,
                                        ip, vp, vp, i64, ip, ip, ip, vp]),
+        "seg_bbox_labels": (ip, [vp, vp, vp, vp, ip, ip, ip, ip, vp, vp]),
+        "seg_tag_labels": (ip, [vp, ip, ip, ip, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

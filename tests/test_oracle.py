@@ -133,3 +133,34 @@ def test_weak_weights_follow_l1_decision():
     dec = L["decisions"]["l1_logits"].numpy()
     assert L["counts"][1] == int((dec == CITYSCAPES["cid_l1_vehicle"]).sum())
     assert L["counts"][2] == 0                            # car boxes are void for the human head
+
+
+def test_label_resize_geometry_known_answers():
+    """resize_images_or_labels(preserve_aspect_ratio=True, mode='max') sizes and the TF 1.12
+    nearest-neighbour source index (utils/utils.py:567-585; align_corners=False)."""
+    from input_pipelines.weak_labels import aspect_preserving_size, nearest_index
+    assert aspect_preserving_size(1024, 2048, 512, 1024) == (512, 1024)
+    assert aspect_preserving_size(375, 500, 512, 1024) == (768, 1024)   # scale = 2.048
+    assert aspect_preserving_size(600, 400, 512, 1024) == (1536, 1024)
+    np.testing.assert_array_equal(nearest_index(7, 7), np.arange(7))
+    np.testing.assert_array_equal(nearest_index(4, 8), [0, 0, 1, 1, 2, 2, 3, 3])
+    np.testing.assert_array_equal(nearest_index(5, 3), [0, 1, 3])       # floor(d * 5/3)
+
+
+def test_bbox_label_map_identity_equals_rasterisation():
+    from input_pipelines.weak_labels import bbox_label_map, generate_bbox_rla
+    cids = np.array([2, 7])
+    coords = np.array([[0.1, 0.6, 0.2, 0.9], [0.5, 1.0, 0.0, 0.4]], np.float32)
+    a = bbox_label_map(cids, coords, (20, 30), (20, 30), (0, 0), (20, 30))
+    np.testing.assert_array_equal(a, generate_bbox_rla(cids, coords, (20, 30)))
+
+
+def test_bbox_coordinates_truncate_the_float64_product():
+    """The reference's int(coord * size) sees numpy's float64 product of a float32 coordinate
+    and an integer size; a float32 product can round up across an integer and move a box
+    edge by one pixel."""
+    from input_pipelines.weak_labels import generate_bbox_rla
+    c = np.float32(0.7)      # c * 10 = 6.99999988 in float64; the float32 product rounds to 7
+    assert int(np.float32(c) * np.float32(10)) == 7 and int(float(c) * 10) == 6
+    rla = generate_bbox_rla([4], np.array([[0.0, c, 0.0, 1.0]], np.float32), (2, 10))
+    assert rla[0, 6, 4] == 1.0 and rla[0, 7, 14] == 1.0
