@@ -23,6 +23,7 @@
 //  * K-tiles run channel-chunk-major, tap-minor, so the KH*KW shifted reads of one chunk's
 //    source rows hit L2 (dilated 3x3: +6 %).
 #include "conv.h"
+#include <cstdlib>
 
 namespace {
 
@@ -58,12 +59,20 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   const int mtiles = (int)((M + BM - 1) / BM);
   const int ntiles = (a.Co + BN - 1) / BN;
   const int nwg = mtiles * ntiles;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int mt = wg / ntiles, nt = wg - mt * ntiles;
-  const long m0 = (long)mt * BM;
-  const int n0 = nt * BN;
+  // persistent: block b runs tiles t = b, b + G, ... (G = gridDim.x, a multiple of 8); the
+  // XCD-aware bijective remap of t (XCD = t % 8 = b % 8) gives each XCD a contiguous run of
+  // tiles, n fastest, so blocks sharing an A panel share an L2
+  auto tile_of = [&](int t, int& mt_, int& nt_) {
+    const int xcd = t & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (t >> 3);
+    mt_ = wg / ntiles;
+    nt_ = wg - mt_ * ntiles;
+  };
+  int tile = blockIdx.x;
+  int mt, nt;
+  tile_of(tile, mt, nt);
+  long m0 = (long)mt * BM;
+  int n0 = nt * BN;
   const int nk = (a.KH * a.KW * a.C) / PBK;
   const int ntaps = a.KH * a.KW;
   const bf16_t* X = (const bf16_t*)a.x;
@@ -83,34 +92,37 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   const int pc = lane & 7;
   int a_voff[4], a_bits[4], a_h0[4], a_w0[4], a_lc[4];
   long a_nb[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
-    const int row = (j >> 1) * 128 + rr;
-    a_lc[j] = swz(rr, pc);
-    const long m = m0 + row;
-    const bool ok = m < M;
-    const long mm = ok ? m : 0;
-    const int wo = (int)(mm % a.Wo);
-    const long t = mm / a.Wo;
-    const int ho = (int)(t % a.Ho);
-    a_nb[j] = (t / a.Ho) * a.H;
-    a_h0[j] = ok ? ho * a.sf - a.pad_h : -(1 << 28);
-    a_w0[j] = wo * a.sf - a.pad_w;
-    a_voff[j] = (((int)(a_nb[j] + a_h0[j]) * a.W + a_w0[j]) * a.ldx + a_lc[j] * 8) * 2;
-    int bits = 0;
-    for (int q = 0; q < a.KH; ++q) bits |= ((unsigned)(a_h0[j] + q * a.dil) < (unsigned)a.H) << q;
-    for (int q = 0; q < a.KW; ++q) bits |= ((unsigned)(a_w0[j] + q * a.dil) < (unsigned)a.W) << (4 + q);
-    a_bits[j] = bits;
-  }
-  // B rows: half g, instruction i -> output channel n0 + g*128 + (i*8+wave)*8 + lane/8
   uint32_t b_voff[4];
+  auto setup_lanes = [&](long m0_, int n0_) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
-    const int co = n0 + (j >> 1) * 128 + rr;
-    b_voff[j] = co < a.Co ? (uint32_t)((co * a.ldw + swz(rr, pc) * 8) * 2) : OOB;
-  }
+    for (int j = 0; j < 4; ++j) {
+      const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
+      const int row = (j >> 1) * 128 + rr;
+      a_lc[j] = swz(rr, pc);
+      const long m = m0_ + row;
+      const bool ok = m < M;
+      const long mm = ok ? m : 0;
+      const int wo = (int)(mm % a.Wo);
+      const long t = mm / a.Wo;
+      const int ho = (int)(t % a.Ho);
+      a_nb[j] = (t / a.Ho) * a.H;
+      a_h0[j] = ok ? ho * a.sf - a.pad_h : -(1 << 28);
+      a_w0[j] = wo * a.sf - a.pad_w;
+      a_voff[j] = (((int)(a_nb[j] + a_h0[j]) * a.W + a_w0[j]) * a.ldx + a_lc[j] * 8) * 2;
+      int bits = 0;
+      for (int q = 0; q < a.KH; ++q) bits |= ((unsigned)(a_h0[j] + q * a.dil) < (unsigned)a.H) << q;
+      for (int q = 0; q < a.KW; ++q) bits |= ((unsigned)(a_w0[j] + q * a.dil) < (unsigned)a.W) << (4 + q);
+      a_bits[j] = bits;
+    }
+    // B rows: half g, instruction i -> output channel n0 + g*128 + (i*8+wave)*8 + lane/8
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
+      const int co = n0_ + (j >> 1) * 128 + rr;
+      b_voff[j] = co < a.Co ? (uint32_t)((co * a.ldw + swz(rr, pc) * 8) * 2) : OOB;
+    }
+  };
+  setup_lanes(m0, n0);
 
   // per-K-tile wave-uniform decode. K-tile order: channel chunk outer, tap inner, so the
   // KH*KW shifted reads of one chunk's source rows follow each other while they are in L2
@@ -158,14 +170,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   };
 
   f32x4_t acc[2][2][4][2];   // [qm][qn][fi][fj]
-#pragma unroll
-  for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   bf16x8_t af[4][2], bfr[2][2];   // [frag][k-half]
   auto read_a = [&](const char* buf, int qm) {
@@ -198,15 +202,29 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // ---- prologue: K-tile 0, halves in issue order A0, B0, B1, A1 ----
-  {
+  // ---- prologue of a tile: K-tile 0, halves in issue order A0, B0, B1, A1 ----
+  auto prologue = [&]() {
+    nx_tap = 0;
+    nx_c0 = 0;
     const KT t0 = ktile_next();
     issue_half(0, t0, 0);
     issue_half(0, t0, 2);
     issue_half(0, t0, 3);
     issue_half(0, t0, 1);
-  }
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // A0, B0 landed (B1, A1 in flight)
+  };
+  prologue();
+  for (;;) {   // ---- persistent tile loop ----
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  // A0, B0 of K-tile 0 landed (B1, A1 in flight; a previous tile's epilogue stores, issued
+  // after them, count too and are waited for here)
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   pp_barrier();
   if (wm == 1) pp_barrier();   // stagger: wave row 1 runs one segment behind
 
@@ -252,9 +270,24 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     if (more && wm == 0) wait_next(true);
     pp_barrier();
   }
-  if (wm == 0) pp_barrier();   // realign the two wave rows
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (wm == 0) pp_barrier();   // realign the two wave rows: every LDS read of the tile is done
+  // next tile: its K-tile 0 goes into buffer 0 now, in flight during this tile's epilogue,
+  // which stages through the buffer-1 region
+  const int tile_n = tile + (int)gridDim.x;
+  const bool has_next = tile_n < nwg;
+  int mt_n = 0, nt_n = 0;
+  if (has_next) {
+    tile_of(tile_n, mt_n, nt_n);
+    setup_lanes((long)mt_n * BM, nt_n * BN);
+    prologue();
+  }
+  // LDS hand-off inside the epilogue: raw barrier after the LDS writes retire (a
+  // __syncthreads would also wait for the next tile's DMA)
+  auto epi_sync = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+  };
+  char* const epi = smem + BUF;
 
   // ---- epilogue (as conv_nt_v2_kernel): flat fragment view fi' = qm*4 + fi, fj' = qn*2 + fj
   constexpr int FM = 8, FN = 4, WMW = 2, WM = 128;
@@ -263,9 +296,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   auto col_of = [&](int fj) { return (fj >> 1) * 128 + wn * 32 + (fj & 1) * 16 + lr; };
   const bool col_writer = lq == 0;
   const int rows_valid = (int)((M - m0) < BM ? (M - m0) : BM);
-  float* red = (float*)smem;
+  float* red = (float*)epi;
   if (a.stats && rows_valid == BM) {
-    float2* red2 = (float2*)smem;
+    float2* red2 = (float2*)epi;
     constexpr float NL = (float)(4 * FM);
     float sj[FN], mj[FN];
 #pragma unroll
@@ -297,7 +330,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     if (col_writer)
 #pragma unroll
       for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
-    __syncthreads();
+    epi_sync();
     if (wm == 0 && col_writer) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -315,7 +348,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = t;
       }
     }
-    __syncthreads();
+    epi_sync();
   } else if (a.stats) {
     float cs[FN];
 #pragma unroll
@@ -332,7 +365,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     if (col_writer)
 #pragma unroll
       for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
-    __syncthreads();
+    epi_sync();
     float mean[FN], tot[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -357,11 +390,11 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
       cs[j] = v;
     }
-    __syncthreads();
+    epi_sync();
     if (col_writer)
 #pragma unroll
       for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
-    __syncthreads();
+    epi_sync();
     if (wm == 0 && col_writer) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -372,9 +405,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = make_float2(tot[j], t);
       }
     }
-    __syncthreads();
+    epi_sync();
   }
-  float* stage = (float*)smem;
+  float* stage = (float*)epi;
   bf16_t* Y = (bf16_t*)a.y;
   const bf16_t* R1 = (const bf16_t*)a.r;
   const bf16_t* R2 = (const bf16_t*)a.r2;
@@ -392,7 +425,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
           for (int k = 0; k < 4; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = A_(i, j)[k];
       }
     }
-    __syncthreads();
+    epi_sync();
     const int n = n0 + cbase + s_cc * 8;
     if (n < a.Co) {
 #pragma unroll
@@ -419,8 +452,15 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         }
       }
     }
-    __syncthreads();
+    epi_sync();
   }
+  if (!has_next) break;
+  tile = tile_n;
+  mt = mt_n;
+  nt = nt_n;
+  m0 = (long)mt * BM;
+  n0 = nt * BN;
+  }   // persistent tile loop
 }
 
 // (the body is a device function: the host pass does not parse buffer-resource values)
@@ -429,19 +469,33 @@ __global__ __launch_bounds__(PP_THREADS, 1) void conv_nt_pp_kernel(ConvArgs a) {
   conv_nt_pp_body<ST>(a);
 }
 
+int pp_grid(int nwg) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    ncu = (ncu + 7) / 8 * 8;   // a multiple of the XCD count keeps tile t on XCD t % 8
+  }
+  const char* e = getenv("SEG_NT_PERSIST");
+  if (e && e[0] == '0') return nwg;   // one tile per workgroup (A/B)
+  return nwg < ncu ? nwg : ncu;
+}
+
 template <int ST>
 hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
-  static_assert(256 * EPI_LD * 4 <= PP_LDS, "epilogue staging fits the ring");
+  constexpr int LDS = BUF + 256 * EPI_LD * 4;   // ring buffer 0 + (buffer 1 | epilogue staging)
+  static_assert(LDS >= PP_LDS && LDS <= 160 * 1024, "LDS budget");
   auto kern = conv_nt_pp_kernel<ST>;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const long M = (long)a.N * a.Ho * a.Wo;
   const int nwg = ceil_div(M, 256) * ceil_div(a.Co, 256);
-  hipLaunchKernelGGL(kern, dim3(nwg), dim3(PP_THREADS), PP_LDS, s, a);
+  hipLaunchKernelGGL(kern, dim3(pp_grid(nwg)), dim3(PP_THREADS), LDS, s, a);
   return hipGetLastError();
 }
 
