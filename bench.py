@@ -181,6 +181,10 @@ def main():
                     "kernel": CLS_NAMES[dom],
                     "launches": r["launches"],
                     "avg_launch_ms": round(r["ms"] / max(r["launches"], 1), 4),
+                    # fwd + dgrad share the conv_nt*_kernel names in a rocprofv3 trace: their
+                    # joint per-launch average is what profiles/*_kernel_classes_*.txt lists
+                    "avg_launch_ms_nt_fwd_dgrad": round((cls[0]["ms"] + cls[1]["ms"]) /
+                                                        max(cls[0]["launches"] + cls[1]["launches"], 1), 4),
                     "share_of_step": round(r["ms"] / (elapsed * 1e3 / args.steps), 3),
                     "profiled_steps": 1,
                     "classes_ms_per_step": {CLS_NAMES[c]: round(cls[c]["ms"], 2) for c in cls},

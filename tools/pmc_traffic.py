@@ -11,8 +11,8 @@ import sqlite3
 import sys
 from collections import defaultdict
 
-CLASSES = {"conv_wgrad": ("conv_wgrad_v2_kernel", "conv_wgrad_kernel"),
-           "conv_nt": ("conv_nt_v2_kernel", "conv_nt_kernel")}
+CLASSES = {"conv_wgrad": ("conv_wgrad_pp_kernel", "conv_wgrad_v2_kernel", "conv_wgrad_kernel"),
+           "conv_nt": ("conv_nt_pp_kernel", "conv_nt_v2_kernel", "conv_nt_kernel")}
 
 
 def per_dispatch(db, counter):
