@@ -100,6 +100,15 @@ int seg_outputs(seg_ctx* ctx, const float** losses, const float** reg,
 int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions, int64_t n,
                   int num_classes, int32_t* cm, void* stream);
 
+/* gradient all-reduce buckets, in the order the backward completes them: n buckets
+ * [lo[i], hi[i]) of the flat [grads | BN stats] buffer (conv-weight ranges cut at layer
+ * boundaries, about SEG_BUCKET_MB = 32 MB each, then the BN-parameter + statistics tail);
+ * returns n (fills at most max_buckets). seg_backward records one event per bucket when its
+ * gradients are written; seg_stream_wait_bucket makes `stream` wait for it (the caller's
+ * collective for bucket i then overlaps the rest of the backward). */
+int seg_grad_buckets(seg_ctx* ctx, int max_buckets, int64_t* lo, int64_t* hi);
+int seg_stream_wait_bucket(seg_ctx* ctx, int bucket, void* stream);
+
 /* weak-label maps on the device (input_subset_bboxes_v2.py:74-98 rasterisation fused with the
  * aspect-preserving nearest-neighbour resize + crop of input_pipelines/utils.py:181-241;
  * input_subset_image_labels.py:73-107 for tags). All pointers are device memory:

@@ -138,6 +138,16 @@ struct seg_ctx {
   float* loss_part = nullptr;
   int loss_blocks = 0;
   float* loss_out = nullptr;      // [10]
+  // gradient all-reduce buckets in ready order: conv-weight ranges [lo, hi) cut at layer
+  // boundaries walking the layers in reverse (the backward's order), then the BN-parameter +
+  // batch-statistics tail. An event is recorded on the backward stream as soon as every
+  // weight gradient of a bucket has been written, so a collective on another stream can
+  // start while the rest of the backward runs.
+  std::vector<long> bk_lo, bk_hi;
+  std::vector<std::vector<int>> bk_convs;
+  std::vector<hipEvent_t> bk_ev;
+  std::vector<char> wg_done;
+  int bk_next = 0;
   float* dzscale = nullptr;       // [ldl]
   float* reg_part = nullptr;
   float* reg_out = nullptr;
@@ -487,7 +497,32 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
   return prof_end(c, S.s, slot);
 }
 
+// record the events of every bucket whose weight gradients are all written (in order)
+int bucket_progress(seg_ctx* c, hipStream_t s, bool final) {
+  const int nw = (int)c->bk_convs.size();
+  while (c->bk_next < (int)c->bk_ev.size()) {
+    const int b = c->bk_next;
+    if (b < nw) {
+      bool ok = true;
+      for (int li : c->bk_convs[b]) ok = ok && c->wg_done[li];
+      if (!ok && !final) return 0;
+    } else if (!final) {
+      return 0;
+    }
+    HIPCALL(c, hipEventRecord(c->bk_ev[b], s));
+    ++c->bk_next;
+  }
+  return 0;
+}
+
+int conv_wgrad_impl(Step& S, int li, const Act& x);
 int conv_wgrad(Step& S, int li, const Act& x) {
+  if (int r = conv_wgrad_impl(S, li, x)) return r;
+  S.c->wg_done[li] = 1;
+  return bucket_progress(S.c, S.s, false);
+}
+
+int conv_wgrad_impl(Step& S, int li, const Act& x) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
   WgradArgs a{};
@@ -654,6 +689,25 @@ int build(seg_ctx* c) {
   for (auto& L : c->convs) { L.mv_off = moff; moff += L.co; }
   c->n_moving = 2 * moff;
   c->n_stats = c->n_moving;
+  {
+    const char* e = getenv("SEG_BUCKET_MB");
+    const long cap = (e ? std::max(1L, atol(e)) : 32L) * (1L << 20) / 4;   // floats per bucket
+    long hi = c->n_decay;
+    std::vector<int> cur;
+    for (int li = (int)c->convs.size() - 1; li >= 0; --li) {
+      cur.push_back(li);
+      const long lo = c->convs[li].w_off;
+      if (hi - lo >= cap || li == 0) {
+        c->bk_lo.push_back(lo); c->bk_hi.push_back(hi); c->bk_convs.push_back(cur);
+        cur.clear();
+        hi = lo;
+      }
+    }
+    c->bk_lo.push_back(c->n_decay); c->bk_hi.push_back(c->n_train + c->n_stats);
+    c->bk_ev.resize(c->bk_lo.size());
+    for (auto& ev : c->bk_ev) HIPCALL(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->wg_done.assign(c->convs.size(), 0);
+  }
   for (auto& L : c->convs) {
     c->pinfo.push_back({L.name + "/weights", L.w_off, (long)L.co * L.k * L.k * L.ci, SEG_PARAM_WEIGHTS, {L.co, L.k, L.k, L.ci}});
     c->pinfo.push_back({L.name + "/BatchNorm/beta", L.b_off, L.co, SEG_PARAM_BETA, {L.co, 1, 1, 1}});
@@ -906,7 +960,16 @@ int forward(Step& S, const float* images) {
   return 0;
 }
 
+int backward_layers(Step& S);
 int backward(Step& S) {
+  seg_ctx* c = S.c;
+  std::fill(c->wg_done.begin(), c->wg_done.end(), 0);
+  c->bk_next = 0;
+  if (int r = backward_layers(S)) return r;
+  return bucket_progress(c, S.s, true);
+}
+
+int backward_layers(Step& S) {
   seg_ctx* c = S.c;
   for (int h = 0; h < 3; ++h) {
     Act gz = logits_slice(c, h);
@@ -1027,6 +1090,7 @@ int seg_destroy(seg_ctx* c) {
   (void)hipSetDevice(c->device);
   for (void* p : c->allocs) (void)hipFree(p);
   for (auto ev : c->prof.ev) (void)hipEventDestroy(ev);
+  for (auto ev : c->bk_ev) (void)hipEventDestroy(ev);
   delete c;
   return 0;
 }
@@ -1177,6 +1241,23 @@ int seg_confusion(seg_ctx* c, const int32_t* labels, const int32_t* decisions, i
   hipError_t e = hipMemsetAsync(cm, 0, (size_t)num_classes * num_classes * 4, s);
   if (e == hipSuccess) e = launch_confusion(labels, decisions, n, num_classes, cm, s);
   if (e != hipSuccess) return hip_fail(c, e, "seg_confusion");
+  return 0;
+}
+
+int seg_grad_buckets(seg_ctx* c, int max_buckets, int64_t* lo, int64_t* hi) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  const int n = (int)c->bk_lo.size();
+  for (int i = 0; i < n && i < max_buckets; ++i) {
+    if (lo) lo[i] = c->bk_lo[i];
+    if (hi) hi[i] = c->bk_hi[i];
+  }
+  return n;
+}
+
+int seg_stream_wait_bucket(seg_ctx* c, int bucket, void* stream) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (bucket < 0 || bucket >= (int)c->bk_ev.size()) return set_err(&c->err, -EINVAL, "bad bucket %d", bucket);
+  HIPCALL(c, hipStreamWaitEvent((hipStream_t)stream, c->bk_ev[bucket], 0));
   return 0;
 }
 

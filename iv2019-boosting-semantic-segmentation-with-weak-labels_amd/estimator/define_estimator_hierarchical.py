@@ -42,13 +42,36 @@ def world_size():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
-def allreduce_grads(ctx):
+def allreduce_grads(ctx, overlap=True):
     """SUM all-reduce of the flat gradient buffer (gradients + BN batch-statistics tail) over
     the process group (RCCL over xGMI on MI355X; gloo on CPU tests). Returns the scale that
-    turns the sum into the tower mean."""
+    turns the sum into the tower mean (applied inside the fused update).
+
+    On GPU contexts the buffer goes bucket by bucket (ctx.grad_buckets(): conv-weight ranges
+    in the order the backward writes them, then the BN tail) on a side stream, each
+    collective waiting only for its bucket's event, so the all-reduce of the head and upper
+    layers overlaps the backward of the lower ones; the compute stream waits for the side
+    stream before the update."""
+    import torch
     import torch.distributed as dist
     n = world_size()
-    if n > 1:
+    if n <= 1:
+        return 1.0
+    buckets = ctx.grad_buckets() if overlap and hasattr(ctx, 'grad_buckets') else None
+    if buckets and ctx.grads.is_cuda:
+        main = torch.cuda.current_stream(ctx.grads.device)
+        comm = getattr(ctx, '_comm_stream', None)
+        if comm is None:
+            comm = ctx._comm_stream = torch.cuda.Stream(ctx.grads.device)
+        for i, (lo, hi) in enumerate(buckets):
+            ctx.wait_bucket(i, comm)
+            with torch.cuda.stream(comm):
+                dist.all_reduce(ctx.grads[lo:hi], op=dist.ReduceOp.SUM)
+        main.wait_stream(comm)
+    elif buckets:
+        for lo, hi in buckets:   # host buffers (gloo): the same bucket order, no streams
+            dist.all_reduce(ctx.grads[lo:hi], op=dist.ReduceOp.SUM)
+    else:
         dist.all_reduce(ctx.grads, op=dist.ReduceOp.SUM)
     return 1.0 / n
 

@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = [
     "seg_profile", "seg_profile_dump",
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
+    "seg_grad_buckets", "seg_stream_wait_bucket",
 ]
 
 PYRAMID = {"none": 0, "psp": 1, "aspp": 2}
@@ -88,6 +89,8 @@ def _load():
         "seg_op_conv_wgrad_cfg": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip,
                                        ip, vp, vp, i64, ip, ip, ip, vp]),
         "seg_bbox_labels": (ip, [vp, vp, vp, vp, ip, ip, ip, ip, vp, vp]),
+        "seg_grad_buckets": (ip, [vp, ip, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+        "seg_stream_wait_bucket": (ip, [vp, ip, vp]),
         "seg_tag_labels": (ip, [vp, ip, ip, ip, vp, vp]),
     }
     for name, (res, args) in sig.items():
@@ -212,6 +215,19 @@ class SegContext:
 
     def backward(self, stream=None):
         check(LIB.seg_backward(self.h, _stream(stream)), self.h)
+
+    def grad_buckets(self):
+        """[(lo, hi)] ranges of self.grads in the order the backward completes them."""
+        n = LIB.seg_grad_buckets(self.h, 0, None, None)
+        if n < 0:
+            check(n, self.h)
+        lo, hi = (ctypes.c_int64 * n)(), (ctypes.c_int64 * n)()
+        check(LIB.seg_grad_buckets(self.h, n, lo, hi) - n, self.h)
+        return [(int(lo[i]), int(hi[i])) for i in range(n)]
+
+    def wait_bucket(self, i, stream):
+        """Make `stream` wait until the last seg_backward has written bucket i."""
+        check(LIB.seg_stream_wait_bucket(self.h, i, _stream(stream)), self.h)
 
     def apply_update(self, lr, momentum=0.9, ema_decay_eff=0.0, grad_scale=1.0, stream=None):
         check(LIB.seg_apply_update(self.h, lr, momentum, ema_decay_eff, grad_scale,

@@ -109,7 +109,7 @@ def _free_port():
     return p
 
 
-def _dp_worker(rank, world, port, q):
+def _dp_worker(rank, world, port, q, bucketed=False):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -117,25 +117,34 @@ def _dp_worker(rank, world, port, q):
     from estimator.define_estimator_hierarchical import allreduce_grads
 
     class Ctx:
-        grads = torch.arange(6, dtype=torch.float32) * (rank + 1)
-    scale = allreduce_grads(Ctx)
-    q.put((rank, scale, (Ctx.grads * scale).tolist()))
+        grads = torch.arange(12, dtype=torch.float32) * (rank + 1)
+
+    class BucketCtx(Ctx):
+        # ready order of a backward: weight ranges from the top down, then the BN tail
+        @staticmethod
+        def grad_buckets():
+            return [(7, 10), (2, 7), (0, 2), (10, 12)]
+    c = BucketCtx if bucketed else Ctx
+    scale = allreduce_grads(c)
+    q.put((rank, scale, (c.grads * scale).tolist()))
     dist.destroy_process_group()
 
 
-def test_gradient_averaging_two_gloo_ranks():
-    """Per-tower gradients are SUM all-reduced then scaled by 1/N (MirroredStrategy mean)."""
+@pytest.mark.parametrize("bucketed", [False, True])
+def test_gradient_averaging_two_gloo_ranks(bucketed):
+    """Per-tower gradients are SUM all-reduced then scaled by 1/N (MirroredStrategy mean);
+    the bucketed path (the order seg_grad_buckets reports) gives the same mean."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, bucketed)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    exp = (np.arange(6) * 1 + np.arange(6) * 2) / 2.0
+    exp = (np.arange(12) * 1 + np.arange(12) * 2) / 2.0
     for _, scale, g in res:
         assert scale == 0.5
         np.testing.assert_allclose(g, exp)
