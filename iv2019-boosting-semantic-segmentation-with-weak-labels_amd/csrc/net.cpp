@@ -148,6 +148,12 @@ struct seg_ctx {
   std::vector<hipEvent_t> bk_ev;
   std::vector<char> wg_done;
   int bk_next = 0;
+  // backward on two streams: every weight gradient runs on `side` (waiting for its layer's
+  // dy on the compute stream), so the dgrad -> BN-backward chain and the wgrads overlap
+  bool side_on = false;
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> ev_dy;   // per conv: dy written on the compute stream
+  hipEvent_t ev_join = nullptr;
   float* dzscale = nullptr;       // [ldl]
   float* reg_part = nullptr;
   float* reg_out = nullptr;
@@ -497,19 +503,16 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
   return prof_end(c, S.s, slot);
 }
 
-// record the events of every bucket whose weight gradients are all written (in order)
-int bucket_progress(seg_ctx* c, hipStream_t s, bool final) {
+// record (on the weight-gradient stream ws) the events of every conv-weight bucket whose
+// gradients are all written, in order; `final` flushes the remaining weight buckets
+int bucket_progress(seg_ctx* c, hipStream_t ws, bool final) {
   const int nw = (int)c->bk_convs.size();
-  while (c->bk_next < (int)c->bk_ev.size()) {
+  while (c->bk_next < nw) {
     const int b = c->bk_next;
-    if (b < nw) {
-      bool ok = true;
-      for (int li : c->bk_convs[b]) ok = ok && c->wg_done[li];
-      if (!ok && !final) return 0;
-    } else if (!final) {
-      return 0;
-    }
-    HIPCALL(c, hipEventRecord(c->bk_ev[b], s));
+    bool ok = true;
+    for (int li : c->bk_convs[b]) ok = ok && c->wg_done[li];
+    if (!ok && !final) return 0;
+    HIPCALL(c, hipEventRecord(c->bk_ev[b], ws));
     ++c->bk_next;
   }
   return 0;
@@ -517,9 +520,16 @@ int bucket_progress(seg_ctx* c, hipStream_t s, bool final) {
 
 int conv_wgrad_impl(Step& S, int li, const Act& x);
 int conv_wgrad(Step& S, int li, const Act& x) {
-  if (int r = conv_wgrad_impl(S, li, x)) return r;
-  S.c->wg_done[li] = 1;
-  return bucket_progress(S.c, S.s, false);
+  seg_ctx* c = S.c;
+  Step W = S;
+  if (c->side_on) {   // the layer's dy (and the wgrad input x) are ready on the compute stream
+    HIPCALL(c, hipEventRecord(c->ev_dy[li], S.s));
+    HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_dy[li], 0));
+    W.s = c->side;
+  }
+  if (int r = conv_wgrad_impl(W, li, x)) return r;
+  c->wg_done[li] = 1;
+  return bucket_progress(c, W.s, false);
 }
 
 int conv_wgrad_impl(Step& S, int li, const Act& x) {
@@ -707,6 +717,14 @@ int build(seg_ctx* c) {
     c->bk_ev.resize(c->bk_lo.size());
     for (auto& ev : c->bk_ev) HIPCALL(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c->wg_done.assign(c->convs.size(), 0);
+    const char* se = getenv("SEG_SIDE_STREAM");
+    c->side_on = !(se && se[0] == '0');
+    if (c->side_on) {
+      HIPCALL(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+      c->ev_dy.resize(c->convs.size());
+      for (auto& ev : c->ev_dy) HIPCALL(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      HIPCALL(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
   }
   for (auto& L : c->convs) {
     c->pinfo.push_back({L.name + "/weights", L.w_off, (long)L.co * L.k * L.k * L.ci, SEG_PARAM_WEIGHTS, {L.co, L.k, L.k, L.ci}});
@@ -965,8 +983,19 @@ int backward(Step& S) {
   seg_ctx* c = S.c;
   std::fill(c->wg_done.begin(), c->wg_done.end(), 0);
   c->bk_next = 0;
+  if (c->side_on) {   // the side stream must not run ahead of the previous use of its buffers
+    HIPCALL(c, hipEventRecord(c->ev_join, S.s));
+    HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
+  }
   if (int r = backward_layers(S)) return r;
-  return bucket_progress(c, S.s, true);
+  if (int r = bucket_progress(c, c->side_on ? c->side : S.s, true)) return r;
+  if (c->side_on) {   // join: the update (and the next forward) follow every weight gradient
+    HIPCALL(c, hipEventRecord(c->ev_join, c->side));
+    HIPCALL(c, hipStreamWaitEvent(S.s, c->ev_join, 0));
+  }
+  // BN-parameter + statistics tail bucket: written on the compute stream
+  HIPCALL(c, hipEventRecord(c->bk_ev.back(), S.s));
+  return 0;
 }
 
 int backward_layers(Step& S) {
@@ -1091,6 +1120,9 @@ int seg_destroy(seg_ctx* c) {
   for (void* p : c->allocs) (void)hipFree(p);
   for (auto ev : c->prof.ev) (void)hipEventDestroy(ev);
   for (auto ev : c->bk_ev) (void)hipEventDestroy(ev);
+  for (auto ev : c->ev_dy) (void)hipEventDestroy(ev);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
   return 0;
 }
