@@ -151,6 +151,7 @@ struct seg_ctx {
   // backward on two streams: every weight gradient runs on `side` (waiting for its layer's
   // dy on the compute stream), so the dgrad -> BN-backward chain and the wgrads overlap
   bool side_on = false;
+  bool side_active = false;        // this backward: side_on and not profiling (kernel-alone timing)
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> ev_dy;   // per conv: dy written on the compute stream
   hipEvent_t ev_join = nullptr;
@@ -522,7 +523,7 @@ int conv_wgrad_impl(Step& S, int li, const Act& x);
 int conv_wgrad(Step& S, int li, const Act& x) {
   seg_ctx* c = S.c;
   Step W = S;
-  if (c->side_on) {   // the layer's dy (and the wgrad input x) are ready on the compute stream
+  if (c->side_active) {   // the layer's dy (and the wgrad input x) are ready on the compute stream
     HIPCALL(c, hipEventRecord(c->ev_dy[li], S.s));
     HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_dy[li], 0));
     W.s = c->side;
@@ -983,13 +984,15 @@ int backward(Step& S) {
   seg_ctx* c = S.c;
   std::fill(c->wg_done.begin(), c->wg_done.end(), 0);
   c->bk_next = 0;
-  if (c->side_on) {   // the side stream must not run ahead of the previous use of its buffers
+  // a profiled backward runs on one stream so the HIP-event kernel timings are kernel-alone
+  c->side_active = c->side_on && !c->prof.on;
+  if (c->side_active) {   // the side stream must not run ahead of the previous use of its buffers
     HIPCALL(c, hipEventRecord(c->ev_join, S.s));
     HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
   }
   if (int r = backward_layers(S)) return r;
-  if (int r = bucket_progress(c, c->side_on ? c->side : S.s, true)) return r;
-  if (c->side_on) {   // join: the update (and the next forward) follow every weight gradient
+  if (int r = bucket_progress(c, c->side_active ? c->side : S.s, true)) return r;
+  if (c->side_active) {   // join: the update (and the next forward) follow every weight gradient
     HIPCALL(c, hipEventRecord(c->ev_join, c->side));
     HIPCALL(c, hipStreamWaitEvent(S.s, c->ev_join, 0));
   }
