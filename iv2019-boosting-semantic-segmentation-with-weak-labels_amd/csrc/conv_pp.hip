@@ -45,7 +45,10 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int ST>
+// PERSIST: loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
+// epilogue; 0 = one tile per workgroup (the residual-epilogue launches: their register
+// budget goes to the residual prefetch instead of the next tile's address state)
+template <int ST, int PERSIST>
 __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   constexpr int BM = 256, BN = 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -274,7 +277,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   // next tile: its K-tile 0 goes into buffer 0 now, in flight during this tile's epilogue,
   // which stages through the buffer-1 region
   const int tile_n = tile + (int)gridDim.x;
-  const bool has_next = tile_n < nwg;
+  const bool has_next = PERSIST && tile_n < nwg;
   int mt_n = 0, nt_n = 0;
   if (has_next) {
     tile_of(tile_n, mt_n, nt_n);
@@ -412,9 +415,35 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   const bf16_t* R1 = (const bf16_t*)a.r;
   const bf16_t* R2 = (const bf16_t*)a.r2;
   const int s_rl = tid >> 3, s_cc = tid & 7;
+  // residual operands (dgrad): one pass's rows are loaded into registers before its
+  // accumulators are staged, all loads unconditional (rows past M clamped), so they are in
+  // flight together with the LDS staging and cost one wait per pass (a per-row conditional
+  // load made hipcc wait vmcnt(0) after every load)
+  // (persistent launches carry no residuals: pp_launch_st routes those to PERSIST = 0)
+  const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
+  auto bf8_add = [](float* v, const uint4 u) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] += bf2f((bf16_t)(w[i] & 0xffff));
+      v[2 * i + 1] += bf2f((bf16_t)(w[i] >> 16));
+    }
+  };
 #pragma unroll
   for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
     const int cbase = pass * EPI_COLS;
+    const int n = n0 + cbase + s_cc * 8;
+    const int nc = n < a.Co ? n : 0;
+    uint4 r1v[BM / 64], r2v[BM / 64];
+    if (nres) {
+#pragma unroll
+      for (int rr = 0; rr < BM / 64; ++rr) {
+        const long m = m0 + s_rl + 64 * rr;
+        const long mc = m < M ? m : M - 1;
+        r1v[rr] = *(const uint4*)(R1 + (size_t)mc * a.ldr + nc);
+        if (nres == 2) r2v[rr] = *(const uint4*)(R2 + (size_t)mc * a.ldr2 + nc);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int col = col_of(j);
@@ -426,31 +455,16 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       }
     }
     epi_sync();
-    const int n = n0 + cbase + s_cc * 8;
-    if (n < a.Co) {
 #pragma unroll
-      for (int rr = 0; rr < BM / 64; ++rr) {
-        const int row = s_rl + 64 * rr;
-        const long m = m0 + row;
-        if (m < M) {
-          const float* sp = stage + row * EPI_LD + s_cc * 8;
-          const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
-          float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-          if (R1) {
-            float u[8];
-            Vec8<bf16_t>::load(R1 + (size_t)m * a.ldr + n, u);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += u[e];
-          }
-          if (R2) {
-            float u[8];
-            Vec8<bf16_t>::load(R2 + (size_t)m * a.ldr2 + n, u);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += u[e];
-          }
-          Vec8<bf16_t>::store(Y + (size_t)m * a.ldy + n, v);
-        }
-      }
+    for (int rr = 0; rr < BM / 64; ++rr) {
+      const int row = s_rl + 64 * rr;
+      const long m = m0 + row;
+      const float* sp = stage + row * EPI_LD + s_cc * 8;
+      const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      if (nres) bf8_add(v, r1v[rr]);
+      if (nres == 2) bf8_add(v, r2v[rr]);
+      if (n < a.Co && m < M) Vec8<bf16_t>::store(Y + (size_t)m * a.ldy + n, v);
     }
     epi_sync();
   }
@@ -464,9 +478,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 }
 
 // (the body is a device function: the host pass does not parse buffer-resource values)
-template <int ST>
+template <int ST, int PERSIST>
 __global__ __launch_bounds__(PP_THREADS, 1) void conv_nt_pp_kernel(ConvArgs a) {
-  conv_nt_pp_body<ST>(a);
+  conv_nt_pp_body<ST, PERSIST>(a);
 }
 
 int pp_grid(int nwg) {
@@ -482,11 +496,11 @@ int pp_grid(int nwg) {
   return nwg < ncu ? nwg : ncu;
 }
 
-template <int ST>
+template <int ST, int PERSIST>
 hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
   constexpr int LDS = BUF + 256 * EPI_LD * 4;   // ring buffer 0 + (buffer 1 | epilogue staging)
   static_assert(LDS >= PP_LDS && LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_nt_pp_kernel<ST>;
+  auto kern = conv_nt_pp_kernel<ST, PERSIST>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -495,8 +509,14 @@ hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
   }
   const long M = (long)a.N * a.Ho * a.Wo;
   const int nwg = ceil_div(M, 256) * ceil_div(a.Co, 256);
-  hipLaunchKernelGGL(kern, dim3(pp_grid(nwg)), dim3(PP_THREADS), LDS, s, a);
+  hipLaunchKernelGGL(kern, dim3(PERSIST ? pp_grid(nwg) : nwg), dim3(PP_THREADS), LDS, s, a);
   return hipGetLastError();
+}
+
+template <int ST>
+hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
+  if (a.r || a.r2) return pp_launch<ST, 0>(a, s);
+  return pp_launch<ST, 1>(a, s);
 }
 
 }  // namespace
@@ -509,8 +529,8 @@ bool conv_nt_pp_ok(const ConvArgs& a) {
 }
 
 hipError_t launch_conv_nt_pp(const ConvArgs& a, hipStream_t s) {
-  if (a.st == 1) return pp_launch<1>(a, s);
-  if (a.st == 2) return pp_launch<2>(a, s);
+  if (a.st == 1) return pp_launch_st<1>(a, s);
+  if (a.st == 2) return pp_launch_st<2>(a, s);
   return hipErrorInvalidValue;
 }
 
