@@ -28,14 +28,14 @@ sys.path[:0] = [REPO, PKG]
 
 H, W, NB = 1024, 2048, 4
 # BASELINE.json configs as per-GPU workloads (4 images per GPU; weak scaling). C4/C5 keep the
-# reference's 1 : 2 : 1 pixel : bbox : tag proportion (train.py:62-64); C5 names fp16 storage,
-# run here in bf16 (same MFMA rate on CDNA4, fp32 exponent range: no loss scaling) with fp32
-# master weights and gradients.
+# reference's 1 : 2 : 1 pixel : bbox : tag proportion (train.py:62-64); C5 runs fp16 storage
+# with fp32 master weights / gradients and dynamic loss scaling (DynamicLossScaler).
 CONFIGS = {
     "C2": {"depth": 50, "mix": (4, 0, 0), "name": "C2: ResNet-50 dilated OS8"},
     "C3": {"depth": 101, "mix": (4, 0, 0), "name": "C3: ResNet-101 dilated OS8"},
     "C4": {"depth": 101, "mix": (2, 2, 0), "name": "C4: ResNet-101 dilated OS8, strong + bbox-weak"},
-    "C5": {"depth": 101, "mix": (1, 2, 1), "name": "C5: ResNet-101 dilated OS8, per-pixel + bbox + tag"},
+    "C5": {"depth": 101, "mix": (1, 2, 1), "dtype": "fp16",
+           "name": "C5: ResNet-101 dilated OS8, per-pixel + bbox + tag, fp16 + fp32 master"},
 }
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
@@ -72,7 +72,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"],
+                    help="storage dtype (default: the config's; fp16 for C5, else bf16)")
     ap.add_argument("--pyramid", default="aspp", choices=["aspp", "psp", "none"])
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
                     help="BASELINE.json workload preset (per-GPU share); C2 is the metric's")
@@ -99,6 +100,8 @@ def main():
 
     cfg = CONFIGS[args.config]
     depth, (nb_pp, nb_pb, nb_pi) = cfg["depth"], cfg["mix"]
+    if args.dtype is None:
+        args.dtype = cfg.get("dtype", "bf16")
     ctx = SegContext(depth=depth, pyramid=args.pyramid, height=H, width=W, nb_pp=nb_pp, nb_pb=nb_pb,
                      nb_pi=nb_pi, dtype=args.dtype, device=local)
     ctx.load_params(init_params(ctx.param_info, seed=0))
@@ -109,15 +112,30 @@ def main():
     tag = torch.as_tensor(data["tag"]).to(dev) if nb_pi else None
     del data
 
+    scaler = None
+    if args.dtype == "fp16":
+        from estimator.define_optimizer import DynamicLossScaler
+        scaler = DynamicLossScaler(ctx)
+
     def step():
         ctx.forward(img)
         ctx.loss(px, bbox, tag)
         ctx.backward()
         scale = allreduce_grads(ctx)
         ctx.apply_update(0.01, 0.9, 0.0, scale)
+        if scaler is not None:
+            scaler.update()   # reads the device overflow flag (one 4-byte copy per step)
 
     for _ in range(args.warmup):
         step()
+    calib = 0
+    if scaler is not None:
+        # the dynamic scale settles before the timed region (untimed extra warmup steps until
+        # four consecutive steps have finite gradients), so the timed steps apply their updates
+        while calib < 32 and scaler.good_steps < 4:
+            step()
+            calib += 1
+        skipped0 = scaler.skipped
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -168,14 +186,14 @@ def main():
                 continue
             conv = c < 3
             ach = r_["gflop"] / r_["ms"]   # GFLOP/ms = TFLOP/s; GB/ms = TB/s
-            pk = (PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS) if conv else PEAK_HBM_TBS
+            pk = (PEAK_BF16_TFLOPS if args.dtype in ("bf16", "fp16") else PEAK_F32_TFLOPS) if conv else PEAK_HBM_TBS
             all_classes[CLS_NAMES[c]] = {"ms": round(r_["ms"], 3), "launches": r_["launches"],
                                          "achieved": round(ach, 2),
                                          "unit": "TFLOP/s" if conv else "TB/s",
                                          "peak": pk, "frac": round(ach / pk, 4)}
         dom = max(cls, key=lambda c: cls[c]["ms"])
         r = cls[dom]
-        peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+        peak = PEAK_BF16_TFLOPS if args.dtype in ("bf16", "fp16") else PEAK_F32_TFLOPS
         achieved = r["gflop"] / r["ms"]  # GFLOP/ms == TFLOP/s
         # HBM bytes per launch of that class from the committed PMC passes of this code
         # (tools/pmc_traffic.sh + tools/pmc_traffic.py; rocprofv3 cannot run inside the bench)
@@ -240,6 +258,9 @@ def main():
                           "image": [H, W], "parallelism": f"dp{world}"},
                "losses_last_step": [round(float(x), 5) for x in lv[:4]],
                "miou_train_summary": miou,
+               "loss_scale": None if scaler is None else {
+                   "scale": scaler.scale, "skipped_warmup": skipped0, "calibration_steps": calib,
+                   "skipped_timed": scaler.skipped - skipped0},
                "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -39,7 +39,7 @@ extern "C" {
 typedef struct seg_ctx seg_ctx;
 
 enum { SEG_PYRAMID_NONE = 0, SEG_PYRAMID_PSP = 1, SEG_PYRAMID_ASPP = 2 };
-enum { SEG_DTYPE_F32 = 0, SEG_DTYPE_BF16 = 1 };
+enum { SEG_DTYPE_F32 = 0, SEG_DTYPE_BF16 = 1, SEG_DTYPE_F16 = 2 };
 enum { SEG_DATASET_CITYSCAPES = 0, SEG_DATASET_VISTAS = 1 };
 enum { SEG_PARAM_WEIGHTS = 0, SEG_PARAM_GAMMA = 1, SEG_PARAM_BETA = 2,
        SEG_PARAM_MOVING_MEAN = 3, SEG_PARAM_MOVING_VAR = 4 };
@@ -99,6 +99,14 @@ int seg_outputs(seg_ctx* ctx, const float** losses, const float** reg,
                 const float** logits_lowres, int* ld_logits, int* h_low, int* w_low);
 int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions, int64_t n,
                   int num_classes, int32_t* cm, void* stream);
+
+/* loss scaling (fp16 storage, BASELINE config C5: fp16 with fp32 master gradients). The
+ * gradient seed of seg_loss is multiplied by `scale`; seg_apply_update first flags non-finite
+ * weight/BN gradients (device int, seg_found_inf), unscales them by grad_scale / scale (the BN
+ * batch-statistics tail by grad_scale only) and skips the parameter update of a flagged step.
+ * The caller adjusts the scale from the flag (dynamic loss scaling). */
+int seg_set_loss_scale(seg_ctx* ctx, float scale);
+int seg_found_inf(seg_ctx* ctx, const int32_t** flag_device);
 
 /* gradient all-reduce buckets, in the order the backward completes them: n buckets
  * [lo[i], hi[i]) of the flat [grads | BN stats] buffer (conv-weight ranges cut at layer

@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void bn_apply8_kernel(BnApplyArgs a) {
         uint32_t bits = 0;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const bool pos = sizeof(TO) == 2 ? f2bf(o[e]) != 0 : o[e] > 0.f;
+          const bool pos = sizeof(TO) == 2 ? TypeOps<TO>::to_f(TypeOps<TO>::from_f(o[e])) > 0.f : o[e] > 0.f;
           bits |= (uint32_t)pos << e;
         }
         a.mask[(size_t)(base + k * L.rpp) * (a.C >> 3) + L.cg] = (uint8_t)bits;
@@ -375,6 +375,11 @@ template <> struct Raw8<bf16_t> {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { o[2 * i] = bf2f((bf16_t)(w[i] & 0xffff)); o[2 * i + 1] = bf2f((bf16_t)(w[i] >> 16)); }
   }
+};
+template <> struct Raw8<f16_t> {
+  uint4 u;
+  __device__ __forceinline__ void load(const f16_t* p) { u = *(const uint4*)p; }
+  __device__ __forceinline__ void cvt(float* o) const { Half<f16_t>::unpack(u, o); }
 };
 template <> struct Raw8<float> {
   float4 a, b;
@@ -639,6 +644,10 @@ hipError_t launch_bn_apply(int dtype, int out_f32, const BnApplyArgs& a, hipStre
     if (out_f32) return apply_t<bf16_t, float>(a, s);
     return apply_t<bf16_t, bf16_t>(a, s);
   }
+  if (dtype == SEG_F16) {
+    if (out_f32) return apply_t<f16_t, float>(a, s);
+    return apply_t<f16_t, f16_t>(a, s);
+  }
   return apply_t<float, float>(a, s);
 }
 
@@ -655,6 +664,10 @@ hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipSt
     if (dz_f32) return bwd_reduce_t<bf16_t, float>(a, s);
     return bwd_reduce_t<bf16_t, bf16_t>(a, s);
   }
+  if (dtype == SEG_F16) {
+    if (dz_f32) return bwd_reduce_t<f16_t, float>(a, s);
+    return bwd_reduce_t<f16_t, f16_t>(a, s);
+  }
   return bwd_reduce_t<float, float>(a, s);
 }
 
@@ -669,6 +682,10 @@ hipError_t launch_bn_bwd_apply(int dtype, int dz_f32, const BnBwdArgs& a, hipStr
   if (dtype == SEG_BF16) {
     if (dz_f32) return bwd_apply_t<bf16_t, float>(a, s);
     return bwd_apply_t<bf16_t, bf16_t>(a, s);
+  }
+  if (dtype == SEG_F16) {
+    if (dz_f32) return bwd_apply_t<f16_t, float>(a, s);
+    return bwd_apply_t<f16_t, f16_t>(a, s);
   }
   return bwd_apply_t<float, float>(a, s);
 }

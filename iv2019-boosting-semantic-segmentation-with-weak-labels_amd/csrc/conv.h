@@ -59,22 +59,22 @@ bool conv_nt_v2_ok(const ConvArgs& a);
 int conv_nt_v2_rows(const ConvArgs& a);   // tile rows (= BN-stat partial rows) of the v2 config
 // true when launch_conv_nt runs the v2 kernel
 bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a);
-hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s);
+hipError_t launch_conv_nt_v2(int dtype, const ConvArgs& a, hipStream_t s);
 // ping-pong 256x256 main loop (conv_pp.hip) for the v2 cases with Co > 128
 bool conv_nt_pp_ok(const ConvArgs& a);
 bool conv_nt_pp_enabled();
-hipError_t launch_conv_nt_pp(const ConvArgs& a, hipStream_t s);
+hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s);
 // ping-pong 256x256 weight gradient (conv_pp.hip), used when the v2 tile choice is 256 x 256
 bool conv_wgrad_pp_ok(const WgradArgs& a);
-hipError_t launch_conv_wgrad_pp(const WgradArgs& a, hipStream_t s);
+hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s);
 bool conv_wgrad_v2_ok(const WgradArgs& a);
-hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s);
-hipError_t launch_conv_wgrad_v2_tile(const WgradArgs& a, int bm, int bn, hipStream_t s);
+hipError_t launch_conv_wgrad_v2(int dtype, const WgradArgs& a, hipStream_t s);
+hipError_t launch_conv_wgrad_v2_tile(int dtype, const WgradArgs& a, int bm, int bn, hipStream_t s);
 void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn);
 
-// 3-channel stem in bf16, laid out as 8-channel taps (tap8 mode):
-//   images f32 [M][3] -> bf16 [M][8] (channels 3..7 zero)
-hipError_t launch_cast_pad8(const float* src, bf16_t* dst, long M, hipStream_t s);
+// 3-channel stem in 16-bit storage, laid out as 8-channel taps (tap8 mode):
+//   images f32 [M][3] -> bf16/fp16 [M][8] (channels 3..7 zero)
+hipError_t launch_cast_pad8(int dtype, const float* src, void* dst, long M, hipStream_t s);
 //   weights bf16 [Co][taps][ci] -> [Co][ldw] with 8-channel taps, zero padded
 hipError_t launch_stem_pad_weights(const bf16_t* w, bf16_t* wp, int co, int taps, int ci, int ldw,
                                    hipStream_t s);

@@ -22,6 +22,7 @@ constexpr int NT_THREADS = 256;
 
 template <typename T> struct MmaT;
 template <> struct MmaT<bf16_t> { static constexpr int BK = 64; };
+template <> struct MmaT<f16_t> { static constexpr int BK = 64; };
 template <> struct MmaT<float> { static constexpr int BK = 32; };
 
 __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
@@ -29,9 +30,11 @@ __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 
 template <typename TO> __device__ __forceinline__ void store_out(TO* p, float v);
 template <> __device__ __forceinline__ void store_out<float>(float* p, float v) { *p = v; }
 template <> __device__ __forceinline__ void store_out<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+template <> __device__ __forceinline__ void store_out<f16_t>(f16_t* p, float v) { *p = (f16_t)v; }
 template <typename TO> __device__ __forceinline__ float round_as(float v);
 template <> __device__ __forceinline__ float round_as<float>(float v) { return v; }
 template <> __device__ __forceinline__ float round_as<bf16_t>(float v) { return bf2f(f2bf(v)); }
+template <> __device__ __forceinline__ float round_as<f16_t>(float v) { return (float)(f16_t)v; }
 
 // ======================================================================================
 // NT kernel
@@ -170,22 +173,22 @@ __global__ __launch_bounds__(NT_THREADS, 2) void conv_nt_kernel(ConvArgs a) {
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8_t af[FM], bfr[FN];
+        typename Half<T>::V af[FM], bfr[FN];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           int row = wm * WM + i * 16 + lr;
-          af[i] = *(const bf16x8_t*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
+          af[i] = *(const typename Half<T>::V*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
         }
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           int row = wn * WN + j * 16 + lr;
-          bfr[j] = *(const bf16x8_t*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
+          bfr[j] = *(const typename Half<T>::V*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = Half<T>::mma(af[i], bfr[j], acc[i][j]);
       }
     } else {
       float af[FM][8], bfr[FN][8];
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(NT_THREADS, 2) void conv_wgrad_kernel(WgradArgs a) 
     const char* B = Bs(buf);
     if constexpr (sizeof(T) == 2) {
       const int q = (lane & 15) >> 2, pq = lane & 3;
-      bf16x8_t af[FM], bfr[FN];
+      typename Half<T>::V af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         int col = wm * WM + i * 16 + 4 * pq;
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(NT_THREADS, 2) void conv_wgrad_kernel(WgradArgs a) 
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = Half<T>::mma(af[i], bfr[j], acc[i][j]);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -616,15 +619,23 @@ hipError_t wg_dispatch(const WgradArgs& a, hipStream_t s) {
 int conv_nt_mtiles(long M) { return ceil_div(M, 128); }
 
 int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a) {
-  return (dtype == SEG_BF16 && !out_f32 && conv_nt_v2_ok(a)) ? conv_nt_v2_rows(a) : 128;
+  return (seg_half(dtype) && !out_f32 && conv_nt_v2_ok(a)) ? conv_nt_v2_rows(a) : 128;
 }
 
 namespace {
-__global__ void cast_pad8_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst, long M) {
+template <typename E>
+__device__ __forceinline__ uint32_t bits16(float v) {
+  const E h = TypeOps<E>::from_f(v);
+  uint16_t b;
+  __builtin_memcpy(&b, &h, 2);
+  return b;
+}
+template <typename E>
+__global__ void cast_pad8_kernel(const float* __restrict__ src, E* __restrict__ dst, long M) {
   for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (long)gridDim.x * blockDim.x) {
     const float* p = src + 3 * m;
-    const uint32_t w0 = (uint32_t)f2bf(p[0]) | ((uint32_t)f2bf(p[1]) << 16);
-    const uint32_t w1 = (uint32_t)f2bf(p[2]);
+    const uint32_t w0 = bits16<E>(p[0]) | (bits16<E>(p[1]) << 16);
+    const uint32_t w1 = bits16<E>(p[2]);
     *(uint4*)(dst + 8 * m) = make_uint4(w0, w1, 0u, 0u);
   }
 }
@@ -650,10 +661,14 @@ __global__ void splitk_reduce_pad8_kernel(const float* __restrict__ part, int sp
 }
 }  // namespace
 
-hipError_t launch_cast_pad8(const float* src, bf16_t* dst, long M, hipStream_t s) {
+hipError_t launch_cast_pad8(int dtype, const float* src, void* dst, long M, hipStream_t s) {
   long g = (M + 255) / 256;
   if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(cast_pad8_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, s, src, dst, M);
+  const dim3 grid((int)(g < 1 ? 1 : g));
+  if (dtype == SEG_F16)
+    hipLaunchKernelGGL(cast_pad8_kernel<f16_t>, grid, dim3(256), 0, s, src, (f16_t*)dst, M);
+  else
+    hipLaunchKernelGGL(cast_pad8_kernel<bf16_t>, grid, dim3(256), 0, s, src, (bf16_t*)dst, M);
   return hipGetLastError();
 }
 hipError_t launch_stem_pad_weights(const bf16_t* w, bf16_t* wp, int co, int taps, int ci, int ldw,
@@ -670,21 +685,26 @@ hipError_t launch_splitk_reduce_pad8(const float* part, int splits, long split_s
 }
 
 bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a) {
-  return dtype == SEG_BF16 && !out_f32 && conv_nt_v2_ok(a);
+  return seg_half(dtype) && !out_f32 && conv_nt_v2_ok(a);
 }
 
 hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t s) {
-  if (conv_nt_uses_v2(dtype, out_f32, a)) return launch_conv_nt_v2(a, s);
+  if (conv_nt_uses_v2(dtype, out_f32, a)) return launch_conv_nt_v2(dtype, a, s);
   if (dtype == SEG_BF16) {
     if (out_f32) return nt_dispatch<bf16_t, float>(a, s);
     return nt_dispatch<bf16_t, bf16_t>(a, s);
+  }
+  if (dtype == SEG_F16) {
+    if (out_f32) return nt_dispatch<f16_t, float>(a, s);
+    return nt_dispatch<f16_t, f16_t>(a, s);
   }
   return nt_dispatch<float, float>(a, s);
 }
 
 hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s) {
-  if (dtype == SEG_BF16 && conv_wgrad_v2_ok(a)) return launch_conv_wgrad_v2(a, s);
+  if (seg_half(dtype) && conv_wgrad_v2_ok(a)) return launch_conv_wgrad_v2(dtype, a, s);
   if (dtype == SEG_BF16) return wg_dispatch<bf16_t>(a, s);
+  if (dtype == SEG_F16) return wg_dispatch<f16_t>(a, s);
   return wg_dispatch<float>(a, s);
 }
 
@@ -700,7 +720,7 @@ hipError_t launch_weight_flip_batched(int dtype, const FlipJob* jobs, int njobs,
                                       hipStream_t s) {
   long g = (total + 255) / 256;
   if (g > 8192) g = 8192;
-  if (dtype == SEG_BF16)
+  if (seg_half(dtype))   // a bit copy: one 16-bit instantiation serves bf16 and fp16
     hipLaunchKernelGGL(weight_flip_batched_kernel<bf16_t>, dim3((int)g), dim3(256), 0, s, jobs, njobs, total);
   else
     hipLaunchKernelGGL(weight_flip_batched_kernel<float>, dim3((int)g), dim3(256), 0, s, jobs, njobs, total);
@@ -711,7 +731,7 @@ hipError_t launch_weight_flip_transpose(int dtype, const void* w, void* wt, int 
                                         int ci, hipStream_t s) {
   long total = (long)co * kh * kw * ci;
   dim3 g(ceil_div(total, 256));
-  if (dtype == SEG_BF16)
+  if (seg_half(dtype))
     hipLaunchKernelGGL(weight_flip_transpose_kernel<bf16_t>, g, dim3(256), 0, s,
                        (const bf16_t*)w, (bf16_t*)wt, co, kh, kw, ci);
   else

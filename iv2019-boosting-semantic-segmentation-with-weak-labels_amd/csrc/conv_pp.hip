@@ -1,4 +1,5 @@
-// bf16 implicit-GEMM convolution, forward + data-gradient, "ping-pong" schedule for gfx950.
+// 16-bit (bf16 / fp16) implicit-GEMM convolution, forward + data-gradient, "ping-pong"
+// schedule for gfx950.
 //
 // Same operands, gather and epilogue as conv_nt_v2_kernel (conv_v2.hip), different main loop:
 //
@@ -28,7 +29,7 @@
 namespace {
 
 constexpr int PP_THREADS = 512;
-constexpr int PBK = 64;                    // bf16 K-elements per K-tile (128-B LDS rows)
+constexpr int PBK = 64;                    // 16-bit K-elements per K-tile (128-B LDS rows)
 constexpr int HALF = 128 * 128;            // one half-tile: 128 rows x 128 B
 constexpr int BUF = 4 * HALF;              // A0 A1 B0 B1
 constexpr int PP_LDS = 2 * BUF;            // 128 KB
@@ -48,8 +49,9 @@ __device__ __forceinline__ void pp_barrier() {
 // PERSIST: loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
 // epilogue; 0 = one tile per workgroup (the residual-epilogue launches: their register
 // budget goes to the residual prefetch instead of the next tile's address state)
-template <int ST, int PERSIST>
+template <typename E, int ST, int PERSIST>
 __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
+  typedef typename Half<E>::V V;
   constexpr int BM = 256, BN = 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -78,8 +80,8 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   int n0 = nt * BN;
   const int nk = (a.KH * a.KW * a.C) / PBK;
   const int ntaps = a.KH * a.KW;
-  const bf16_t* X = (const bf16_t*)a.x;
-  const bf16_t* Wt = (const bf16_t*)a.w;
+  const E* X = (const E*)a.x;
+  const E* Wt = (const E*)a.w;
 
   // ---- operand addressing: buffer resources, 32-bit byte offsets per lane ----
   // Out-of-range taps and rows get the offset OOB (>= num_records): the buffer unit returns
@@ -174,14 +176,14 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 
   f32x4_t acc[2][2][4][2];   // [qm][qn][fi][fj]
 
-  bf16x8_t af[4][2], bfr[2][2];   // [frag][k-half]
+  V af[4][2], bfr[2][2];   // [frag][k-half]
   auto read_a = [&](const char* buf, int qm) {
     const char* A = buf + qm * HALF;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = wm * 64 + i * 16 + lr;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) af[i][s] = *(const bf16x8_t*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
+      for (int s = 0; s < 2; ++s) af[i][s] = *(const V*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
     }
   };
   auto read_b = [&](const char* buf, int qn) {
@@ -190,7 +192,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     for (int j = 0; j < 2; ++j) {
       const int row = wn * 32 + j * 16 + lr;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) bfr[j][s] = *(const bf16x8_t*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
+      for (int s = 0; s < 2; ++s) bfr[j][s] = *(const V*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
     }
   };
   auto mfma_q = [&](int qm, int qn) {
@@ -201,7 +203,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[qm][qn][i][j], 0, 0, 0);
+          acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfr[j][s], acc[qm][qn][i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -411,9 +413,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     epi_sync();
   }
   float* stage = (float*)epi;
-  bf16_t* Y = (bf16_t*)a.y;
-  const bf16_t* R1 = (const bf16_t*)a.r;
-  const bf16_t* R2 = (const bf16_t*)a.r2;
+  E* Y = (E*)a.y;
+  const E* R1 = (const E*)a.r;
+  const E* R2 = (const E*)a.r2;
   const int s_rl = tid >> 3, s_cc = tid & 7;
   // residual operands (dgrad): one pass's rows are loaded into registers before its
   // accumulators are staged, all loads unconditional (rows past M clamped), so they are in
@@ -422,12 +424,10 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   // (persistent launches carry no residuals: pp_launch_st routes those to PERSIST = 0)
   const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
   auto bf8_add = [](float* v, const uint4 u) {
-    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+    float w[8];
+    Half<E>::unpack(u, w);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] += bf2f((bf16_t)(w[i] & 0xffff));
-      v[2 * i + 1] += bf2f((bf16_t)(w[i] >> 16));
-    }
+    for (int i = 0; i < 8; ++i) v[i] += w[i];
   };
 #pragma unroll
   for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
@@ -464,7 +464,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
       if (nres) bf8_add(v, r1v[rr]);
       if (nres == 2) bf8_add(v, r2v[rr]);
-      if (n < a.Co && m < M) Vec8<bf16_t>::store(Y + (size_t)m * a.ldy + n, v);
+      if (n < a.Co && m < M) Vec8<E>::store(Y + (size_t)m * a.ldy + n, v);
     }
     epi_sync();
   }
@@ -478,9 +478,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 }
 
 // (the body is a device function: the host pass does not parse buffer-resource values)
-template <int ST, int PERSIST>
+template <typename E, int ST, int PERSIST>
 __global__ __launch_bounds__(PP_THREADS, 1) void conv_nt_pp_kernel(ConvArgs a) {
-  conv_nt_pp_body<ST, PERSIST>(a);
+  conv_nt_pp_body<E, ST, PERSIST>(a);
 }
 
 int pp_grid(int nwg) {
@@ -496,11 +496,11 @@ int pp_grid(int nwg) {
   return nwg < ncu ? nwg : ncu;
 }
 
-template <int ST, int PERSIST>
+template <typename E, int ST, int PERSIST>
 hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
   constexpr int LDS = BUF + 256 * EPI_LD * 4;   // ring buffer 0 + (buffer 1 | epilogue staging)
   static_assert(LDS >= PP_LDS && LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_nt_pp_kernel<ST, PERSIST>;
+  auto kern = conv_nt_pp_kernel<E, ST, PERSIST>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -513,10 +513,10 @@ hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int ST>
+template <typename E, int ST>
 hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
-  if (a.r || a.r2) return pp_launch<ST, 0>(a, s);
-  return pp_launch<ST, 1>(a, s);
+  if (a.r || a.r2) return pp_launch<E, ST, 0>(a, s);
+  return pp_launch<E, ST, 1>(a, s);
 }
 
 }  // namespace
@@ -528,14 +528,20 @@ bool conv_nt_pp_ok(const ConvArgs& a) {
          (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31) && (long)a.Co * a.ldw * 2 < (1L << 31);
 }
 
-hipError_t launch_conv_nt_pp(const ConvArgs& a, hipStream_t s) {
-  if (a.st == 1) return pp_launch_st<1>(a, s);
-  if (a.st == 2) return pp_launch_st<2>(a, s);
+template <typename E>
+hipError_t nt_pp_e(const ConvArgs& a, hipStream_t s) {
+  if (a.st == 1) return pp_launch_st<E, 1>(a, s);
+  if (a.st == 2) return pp_launch_st<E, 2>(a, s);
   return hipErrorInvalidValue;
 }
 
+hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s) {
+  if (dtype == SEG_F16) return nt_pp_e<f16_t>(a, s);
+  return nt_pp_e<bf16_t>(a, s);
+}
+
 // ======================================================================================
-// bf16 weight gradient, ping-pong schedule: C[co][tap*Ci+ci] = sum_p dy[p][co] * x[src(p,tap)][ci]
+// 16-bit weight gradient, ping-pong schedule: C[co][tap*Ci+ci] = sum_p dy[p][co] * x[src(p,tap)][ci]
 //
 // The NT kernel's main loop transposed to the TN problem of conv_wgrad_v2_kernel: 256 (co) x
 // 256 (tap,ci) tile, 8 waves as 2 x 4 with 128 x 64 wave tiles in four 64 x 32 quadrants; a
@@ -553,8 +559,9 @@ constexpr int WPP_LDS = 2 * WBUF;
 
 __device__ __forceinline__ int wpp_swz(int row, int ch) { return ch ^ (2 * (row & 3) + 8 * ((row >> 3) & 1)); }
 
-template <int FAST>   // FAST: Wo >= 64 (a K-tile's rows need at most one row carry)
+template <typename E, int FAST>   // FAST: Wo >= 64 (a K-tile's rows need at most one row carry)
 __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
+  typedef typename Half<E>::V V;
   constexpr int BM = 256, BN = 256, PK = 64;
   constexpr uint32_t OOB = 0x80000000u;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -699,7 +706,7 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) b_rb[j] = tr_base(wn * 32 + j * 16 + 4 * p4);
   typedef short s16x8_t __attribute__((ext_vector_type(8)));
-  auto frag2 = [&](uint32_t addr, bf16x8_t& f0, bf16x8_t& f1) {   // k-substeps 0 and 1
+  auto frag2 = [&](uint32_t addr, V& f0, V& f1) {   // k-substeps 0 and 1
     s16x4_t l0, h0, l1, h1;
     asm volatile("ds_read_b64_tr_b16 %0, %4\n\t"
                  "ds_read_b64_tr_b16 %1, %4 offset:1024\n\t"
@@ -711,7 +718,7 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
     __builtin_memcpy(&f0, &v0, 16);
     __builtin_memcpy(&f1, &v1, 16);
   };
-  bf16x8_t af[4][2], bfr[2][2];
+  V af[4][2], bfr[2][2];
   auto read_a = [&](int kb, int qm) {
     const uint32_t off = smem_lds + (kb & 1) * WBUF + qm * WHALF;
 #pragma unroll
@@ -732,7 +739,7 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[qm][qn][i][j], 0, 0, 0);
+          acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfr[j][s], acc[qm][qn][i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
   auto wait_next = [&](bool more) {
@@ -803,9 +810,9 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
         }
 }
 
-template <int FAST>
+template <typename E, int FAST>
 __global__ __launch_bounds__(PP_THREADS, 1) void conv_wgrad_pp_kernel(WgradArgs a) {
-  conv_wgrad_pp_body<FAST>(a);
+  conv_wgrad_pp_body<E, FAST>(a);
 }
 
 }  // namespace
@@ -817,7 +824,7 @@ bool conv_wgrad_pp_ok(const WgradArgs& a) {
          P * a.lddy * 2 < (1L << 31) && (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31);
 }
 
-hipError_t launch_conv_wgrad_pp(const WgradArgs& a, hipStream_t s) {
+hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s) {
   const int Ncol = a.KH * a.KW * a.C;
   const int nwg = ceil_div(a.Co, 256) * ceil_div(Ncol, 256) * a.splits;
   auto launch = [&](auto kern) -> hipError_t {
@@ -826,6 +833,10 @@ hipError_t launch_conv_wgrad_pp(const WgradArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(PP_THREADS), WPP_LDS, s, a);
     return hipGetLastError();
   };
-  if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<1>);
-  return launch(conv_wgrad_pp_kernel<0>);
+  if (dtype == SEG_F16) {
+    if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<f16_t, 1>);
+    return launch(conv_wgrad_pp_kernel<f16_t, 0>);
+  }
+  if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<bf16_t, 1>);
+  return launch(conv_wgrad_pp_kernel<bf16_t, 0>);
 }

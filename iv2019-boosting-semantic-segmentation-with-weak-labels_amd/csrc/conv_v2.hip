@@ -67,9 +67,10 @@ template <> struct AccOf<16> { typedef f32x4_t T; static constexpr int N = 4; };
 // MF: MFMA shape (16: v_mfma_f32_16x16x32_bf16). A v_mfma_f32_32x32x16_bf16 main loop with
 // fragments double-buffered across k16-steps was measured 5-9 % slower on the C2 layer shapes
 // and removed; the epilogue keeps the shape-generic (row_of / col_of) accumulator walk.
-template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM_ = 256>
+template <typename E, int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM_ = 256>
 __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_kernel(ConvArgs a) {
-  const bf16_t* zero = g_zero16;
+  typedef typename Half<E>::V V;
+  const E* zero = (const E*)g_zero16;
   constexpr int BM = BM_;
   constexpr int WM = BM / WMW, WN = BN / WNW;
   constexpr int FM = WM / MF, FN = WN / MF;
@@ -106,8 +107,8 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
   const int n0 = nt * BN;
   const int K = a.KH * a.KW * a.C;
   const int nk = T8 ? (K + BK - 1) / BK : K / BK;   // T8: taps beyond KH*KW read zeros
-  const bf16_t* X = (const bf16_t*)a.x;
-  const bf16_t* Wt = (const bf16_t*)a.w;
+  const E* X = (const E*)a.x;
+  const E* Wt = (const E*)a.w;
 
   // ---- per-lane A rows (fixed over K): image base and the tap-independent coordinates ----
   constexpr int AR = AI;          // A rows per lane per K-step
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
       const int row = (i * 8 + wave) * 8 + (lane >> 3);
       const int co = n0 + row;
       const int lc = swz(row, pc);
-      const bf16_t* src = co < a.Co ? Wt + (size_t)co * a.ldw + k0 + lc * 8 : zero;
+      const E* src = co < a.Co ? Wt + (size_t)co * a.ldw + k0 + lc * 8 : zero;
       glds16(src, sB + (i * 8 + wave) * 1024);
     }
   };
@@ -205,16 +206,16 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
         if (s == 0) issue_a(nkb, nstage);
         else issue_b(nkb, nstage);
       }
-      bf16x8_t af[FM], bfr[FN];
+      V af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * WM + i * 16 + lr;
-        af[i] = *(const bf16x8_t*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
+        af[i] = *(const V*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * WN + j * 16 + lr;
-        bfr[j] = *(const bf16x8_t*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
+        bfr[j] = *(const V*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
       }
 #if SEG_MFMA_PRIO
       __builtin_amdgcn_s_setprio(1);
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = Half<E>::mma(af[i], bfr[j], acc[i][j]);
 #if SEG_MFMA_PRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
@@ -371,9 +372,9 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
   }
   // coalesced stores: fp32 tile staged through LDS 64 columns at a time, 16 B per lane
   float* stage = (float*)smem;
-  bf16_t* Y = (bf16_t*)a.y;
-  const bf16_t* R1 = (const bf16_t*)a.r;
-  const bf16_t* R2 = (const bf16_t*)a.r2;
+  E* Y = (E*)a.y;
+  const E* R1 = (const E*)a.r;
+  const E* R2 = (const E*)a.r2;
   const int s_rl = tid >> 3, s_cc = tid & 7;   // store phase: row lane (0..63), 8-col chunk
 #pragma unroll
   for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
@@ -403,17 +404,17 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
           float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
           if (R1) {
             float u[8];
-            Vec8<bf16_t>::load(R1 + (size_t)m * a.ldr + n, u);
+            Vec8<E>::load(R1 + (size_t)m * a.ldr + n, u);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += u[e];
           }
           if (R2) {
             float u[8];
-            Vec8<bf16_t>::load(R2 + (size_t)m * a.ldr2 + n, u);
+            Vec8<E>::load(R2 + (size_t)m * a.ldr2 + n, u);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += u[e];
           }
-          Vec8<bf16_t>::store(Y + (size_t)m * a.ldy + n, v);
+          Vec8<E>::store(Y + (size_t)m * a.ldy + n, v);
         }
       }
     }
@@ -421,13 +422,13 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
   }
 }
 
-template <int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM = 256>
+template <typename E, int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM = 256>
 hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
   constexpr int STAGE_BYTES = (BM + BN) * 128;
   constexpr int EPI = BM * (64 + 4) * 4;
   constexpr int LDS = STAGES * STAGE_BYTES > EPI ? STAGES * STAGE_BYTES : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_nt_v2_kernel<BN, WMW, WNW, STAGES, ST, T8, MF, BM>;
+  auto kern = conv_nt_v2_kernel<E, BN, WMW, WNW, STAGES, ST, T8, MF, BM>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -469,21 +470,27 @@ int conv_nt_v2_rows(const ConvArgs& a) {
   return 256;
 }
 
-template <int ST>
-hipError_t v2_dispatch(const ConvArgs& a, hipStream_t s) {
+template <typename E, int ST>
+hipError_t v2_dispatch(int dtype, const ConvArgs& a, hipStream_t s) {
   if (a.Co > 128) {
-    if (conv_nt_pp_enabled() && conv_nt_pp_ok(a)) return launch_conv_nt_pp(a, s);
-    return v2_launch<256, 4, 2, 2, ST>(a, s);
+    if (conv_nt_pp_enabled() && conv_nt_pp_ok(a)) return launch_conv_nt_pp(dtype, a, s);
+    return v2_launch<E, 256, 4, 2, 2, ST>(a, s);
   }
-  if (a.Co > 64) return v2_launch<128, 4, 2, 3, ST>(a, s);
-  return v2_launch<64, 8, 1, 3, ST>(a, s);
+  if (a.Co > 64) return v2_launch<E, 128, 4, 2, 3, ST>(a, s);
+  return v2_launch<E, 64, 8, 1, 3, ST>(a, s);
 }
 
-hipError_t launch_conv_nt_v2(const ConvArgs& a, hipStream_t s) {
-  if (a.tap8) return v2_launch<64, 8, 1, 3, 1, 1>(a, s);
-  if (a.st == 1) return v2_dispatch<1>(a, s);
-  if (a.st == 2) return v2_dispatch<2>(a, s);
+template <typename E>
+hipError_t nt_v2_e(int dtype, const ConvArgs& a, hipStream_t s) {
+  if (a.tap8) return v2_launch<E, 64, 8, 1, 3, 1, 1>(a, s);
+  if (a.st == 1) return v2_dispatch<E, 1>(dtype, a, s);
+  if (a.st == 2) return v2_dispatch<E, 2>(dtype, a, s);
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_conv_nt_v2(int dtype, const ConvArgs& a, hipStream_t s) {
+  if (dtype == SEG_F16) return nt_v2_e<f16_t>(dtype, a, s);
+  return nt_v2_e<bf16_t>(dtype, a, s);
 }
 
 // ======================================================================================
@@ -508,7 +515,7 @@ __device__ __forceinline__ int wswz(int row, int ch) {
   else return ch ^ (2 * (row & 3));
 }
 
-template <int BM, int BN, int WMW, int WNW, int STAGES, int WBK>
+template <typename E, int BM, int BN, int WMW, int WNW, int STAGES, int WBK>
 __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs a) {
   constexpr int ROWB_A = BM * 2, ROWB_B = BN * 2;            // bytes per pixel row
   constexpr int CPR_A = BM / 8, CPR_B = BN / 8;              // 16-B chunks per row
@@ -546,9 +553,10 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   const int p_begin = split * chunk;
   const int p_end = (p_begin + chunk < P) ? p_begin + chunk : P;
   const int nk = p_end > p_begin ? (p_end - p_begin + WBK - 1) / WBK : 0;
-  const bf16_t* DY = (const bf16_t*)a.dy;
-  const bf16_t* X = (const bf16_t*)a.x;
-  const bf16_t* zero = g_zero16;
+  typedef typename Half<E>::V V;
+  const E* DY = (const E*)a.dy;
+  const E* X = (const E*)a.x;
+  const E* zero = (const E*)g_zero16;
 
   // ---- launch-invariant per-lane decode ----
   int a_row[AI], a_co[AI];
@@ -639,7 +647,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
 #pragma unroll
     for (int s = 0; s < WBK / 32; ++s) {     // 32-pixel MFMA k-steps per stage
       const int kr = 32 * s + 8 * lq + q4;
-      bf16x8_t af[FM], bfr[FN];
+      V af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int col = wm * WM + i * 16 + 4 * p4;
@@ -665,7 +673,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = Half<E>::mma(af[i], bfr[j], acc[i][j]);
 #if SEG_MFMA_PRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
@@ -709,12 +717,12 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
     }
 }
 
-template <int BM, int BN, int WMW, int WNW, int STAGES, int WBK = 64>
+template <typename E, int BM, int BN, int WMW, int WNW, int STAGES, int WBK = 64>
 hipError_t wg2_launch(const WgradArgs& a, hipStream_t s) {
   constexpr int LDS = STAGES * WBK * (BM + BN) * 2;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(STAGES <= 4 && (STAGES < 4 || 2 * (WBK * (BM + BN) / 8 / WG_THREADS) <= 16), "vmcnt");
-  auto kern = conv_wgrad_v2_kernel<BM, BN, WMW, WNW, STAGES, WBK>;
+  auto kern = conv_wgrad_v2_kernel<E, BM, BN, WMW, WNW, STAGES, WBK>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -752,26 +760,32 @@ void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn) {
   *bn = n;
 }
 
-hipError_t launch_conv_wgrad_v2(const WgradArgs& a, hipStream_t s) {
+hipError_t launch_conv_wgrad_v2(int dtype, const WgradArgs& a, hipStream_t s) {
   int bm, bn;
   conv_wgrad_v2_tile(a.Co, a.KH * a.KW * a.C, (long)a.N * a.Ho * a.Wo, &bm, &bn);
-  return launch_conv_wgrad_v2_tile(a, bm, bn, s);
+  return launch_conv_wgrad_v2_tile(dtype, a, bm, bn, s);
 }
 
 // explicit tile (bm, bn in {64, 128, 256}); 256 x 256 runs the ping-pong kernel
-hipError_t launch_conv_wgrad_v2_tile(const WgradArgs& a, int bm, int bn, hipStream_t s) {
+template <typename E>
+hipError_t wgrad_v2_tile_e(int dtype, const WgradArgs& a, int bm, int bn, hipStream_t s) {
   if (bm == 64) {
-    if (bn == 64) return wg2_launch<64, 64, 4, 2, 3>(a, s);
-    if (bn == 128) return wg2_launch<64, 128, 2, 4, 3>(a, s);
-    return wg2_launch<64, 256, 2, 4, 3>(a, s);
+    if (bn == 64) return wg2_launch<E, 64, 64, 4, 2, 3>(a, s);
+    if (bn == 128) return wg2_launch<E, 64, 128, 2, 4, 3>(a, s);
+    return wg2_launch<E, 64, 256, 2, 4, 3>(a, s);
   }
   if (bm == 128) {
-    if (bn == 64) return wg2_launch<128, 64, 4, 2, 3>(a, s);
-    if (bn == 128) return wg2_launch<128, 128, 4, 2, 3>(a, s);
-    return wg2_launch<128, 256, 2, 4, 3>(a, s);
+    if (bn == 64) return wg2_launch<E, 128, 64, 4, 2, 3>(a, s);
+    if (bn == 128) return wg2_launch<E, 128, 128, 4, 2, 3>(a, s);
+    return wg2_launch<E, 128, 256, 2, 4, 3>(a, s);
   }
-  if (bn == 64) return wg2_launch<256, 64, 8, 1, 3>(a, s);
-  if (bn == 128) return wg2_launch<256, 128, 4, 2, 3>(a, s);
-  if (conv_nt_pp_enabled() && conv_wgrad_pp_ok(a)) return launch_conv_wgrad_pp(a, s);
-  return wg2_launch<256, 256, 2, 4, 2>(a, s);
+  if (bn == 64) return wg2_launch<E, 256, 64, 8, 1, 3>(a, s);
+  if (bn == 128) return wg2_launch<E, 256, 128, 4, 2, 3>(a, s);
+  if (conv_nt_pp_enabled() && conv_wgrad_pp_ok(a)) return launch_conv_wgrad_pp(dtype, a, s);
+  return wg2_launch<E, 256, 256, 2, 4, 2>(a, s);
+}
+
+hipError_t launch_conv_wgrad_v2_tile(int dtype, const WgradArgs& a, int bm, int bn, hipStream_t s) {
+  if (dtype == SEG_F16) return wgrad_v2_tile_e<f16_t>(dtype, a, bm, bn, s);
+  return wgrad_v2_tile_e<bf16_t>(dtype, a, bm, bn, s);
 }

@@ -38,6 +38,7 @@ hipError_t launch_loss_head(const LossArgs& a, const LossTables& t, hipStream_t 
 // out[0..9] = {seg, l1, l2v, l2h, n1, n2v, n2h, f1, f2v, f2h}; dzscale[ldl] per-channel
 // factors (1/n1 | 0.1/n2v | 0.1/n2h; 0 where the count is 0)
 hipError_t launch_loss_finalize(const float* part, int nblocks, const LossTables& t, int ldl,
+                                float loss_scale,
                                 float* out, float* dzscale, hipStream_t s);
 hipError_t launch_confusion(const int* labels, const int* decisions, long n, int num_classes,
                             int* cm, hipStream_t s);

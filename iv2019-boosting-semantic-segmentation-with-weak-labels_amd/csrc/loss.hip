@@ -357,7 +357,7 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
 }
 
 __global__ void loss_finalize_kernel(const float* __restrict__ part, int nblocks, int c1, int c2,
-                                     int c3, int ldl, float* out, float* dzscale) {
+                                     int c3, int ldl, float* out, float* dzscale, float loss_scale) {
   __shared__ double sh[6][256];
   double v[6] = {0, 0, 0, 0, 0, 0};
   for (int b = threadIdx.x; b < nblocks; b += 256)
@@ -388,7 +388,7 @@ __global__ void loss_finalize_kernel(const float* __restrict__ part, int nblocks
     if (c < c1) S = sh[3][0] > 0 ? 1.0 / sh[3][0] : 0.0;
     else if (c < c1 + c2) S = sh[4][0] > 0 ? 0.1 / sh[4][0] : 0.0;
     else if (c < c1 + c2 + c3) S = sh[5][0] > 0 ? 0.1 / sh[5][0] : 0.0;
-    dzscale[c] = (float)S;
+    dzscale[c] = (float)(S * loss_scale);   // the gradient seed carries the loss scale (fp16)
   }
 }
 
@@ -424,9 +424,10 @@ hipError_t launch_loss_head(const LossArgs& a, const LossTables& t, hipStream_t 
 }
 
 hipError_t launch_loss_finalize(const float* part, int nblocks, const LossTables& t, int ldl,
+                                float loss_scale,
                                 float* out, float* dzscale, hipStream_t s) {
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, nblocks, t.c1, t.c2,
-                     t.c3, ldl, out, dzscale);
+                     t.c3, ldl, out, dzscale, loss_scale);
   return hipGetLastError();
 }
 

@@ -82,6 +82,10 @@ struct Prof {
 
 }  // namespace
 
+static int dt_of(int abi_dtype) {
+  return abi_dtype == SEG_DTYPE_BF16 ? SEG_BF16 : (abi_dtype == SEG_DTYPE_F16 ? SEG_F16 : SEG_F32);
+}
+
 struct seg_ctx {
   seg_cfg cfg{};
   int device = 0;
@@ -150,6 +154,8 @@ struct seg_ctx {
   int bk_next = 0;
   // backward on two streams: every weight gradient runs on `side` (waiting for its layer's
   // dy on the compute stream), so the dgrad -> BN-backward chain and the wgrads overlap
+  float loss_scale = 1.f;         // gradient seed multiplier (fp16 dynamic loss scaling)
+  int* skip_flag = nullptr;       // device: non-finite scaled gradients this step (update skipped)
   bool side_on = false;
   bool side_active = false;        // this backward: side_on and not profiling (kernel-alone timing)
   hipStream_t side = nullptr;
@@ -440,7 +446,7 @@ int bn_apply(Step& S, int li, const Act& out, int out_f32, const Act* res = null
   }
   a.out = out.p; a.ldo = out.ld;
   a.mask = a.relu ? out.mask : nullptr;
-  const double esz = S.dt == SEG_BF16 ? 2.0 : 4.0;
+  const double esz = seg_half(S.dt) ? 2.0 : 4.0;
   const double gb = a.M * (double)a.C * (esz * (1 + (a.res || a.y2 ? 1 : 0)) +
                                          (out_f32 ? 4.0 : esz)) * 1e-9;
   int slot;
@@ -465,7 +471,7 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   if (dyhat_out) { a.dyhat = dyhat_out->p; a.lddyhat = dyhat_out->ld; }
   a.part = L.bwd_part; a.rb = L.rb;
   a.dzscale = dzscale;
-  const double esz = S.dt == SEG_BF16 ? 2.0 : 4.0, zsz = dz_f32 ? 4.0 : esz;
+  const double esz = seg_half(S.dt) ? 2.0 : 4.0, zsz = dz_f32 ? 4.0 : esz;
   const double me = a.M * (double)a.C * 1e-9;
   const double gb_in = me * (zsz + (a.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
   int slot;
@@ -737,7 +743,7 @@ int build(seg_ctx* c) {
 
   // ---- activations ----
   const int H = g.height, W = g.width;
-  c->stem8 = c->dt == SEG_BF16;
+  c->stem8 = seg_half(c->dt);
   if (c->stem8)
     if (int r = alloc_act(c, c->img, N, H, W, 8)) return r;
   c->img.N = N; c->img.H = H; c->img.W = W; c->img.C = 3; c->img.ld = c->stem8 ? 8 : 3;
@@ -832,7 +838,7 @@ int build(seg_ctx* c) {
   if (int r = dalloc(c, &c->reg_out, 4)) return r;
 
   // ---- compute weight copies and workspace ----
-  if (c->dt == SEG_BF16)
+  if (seg_half(c->dt))
     if (int r = dalloc(c, (bf16_t**)&c->w_lp_flat, c->n_decay)) return r;
   size_t slab = 0;
   for (auto& L : c->convs) {
@@ -841,7 +847,7 @@ int build(seg_ctx* c) {
       if (int r = dalloc(c, &p, (size_t)L.co * L.k * L.k * L.ci * c->esz)) return r;
       L.wt_lp = p;
     }
-    if (c->dt == SEG_BF16) L.w_lp = (bf16_t*)c->w_lp_flat + L.w_off;
+    if (seg_half(c->dt)) L.w_lp = (uint16_t*)c->w_lp_flat + L.w_off;   // bf16 or fp16 bits
     const int wci = (&L == &c->convs[c->stem] && c->stem8) ? 8 : L.ci;
     slab = std::max(slab, (size_t)wgrad_splits(L, wci) * L.co_pad * L.k * L.k * wci);
   }
@@ -918,9 +924,9 @@ Act logits_slice(seg_ctx* c, int h) {
 int forward(Step& S, const float* images) {
   seg_ctx* c = S.c;
   if (c->stem8) {
-    HIPCALL(c, launch_cast_pad8(images, (bf16_t*)c->img.p, c->img.M(), S.s));
-  } else if (c->dt == SEG_BF16) {
-    HIPCALL(c, launch_cast_f32_bf16(images, (bf16_t*)c->img.p, c->img.M() * 3, S.s));
+    HIPCALL(c, launch_cast_pad8(S.dt, images, c->img.p, c->img.M(), S.s));
+  } else if (seg_half(c->dt)) {
+    HIPCALL(c, launch_cast_f32_half(c->dt, images, c->img.p, c->img.M() * 3, S.s));
   } else {
     c->img.p = (void*)images;
   }
@@ -1082,8 +1088,8 @@ int refresh_stem_pad(seg_ctx* c, hipStream_t s) {
 }
 
 int refresh_compute_weights(seg_ctx* c, hipStream_t s) {
-  if (c->dt == SEG_BF16)
-    HIPCALL(c, launch_cast_f32_bf16(c->params, (bf16_t*)c->w_lp_flat, c->n_decay, s));
+  if (seg_half(c->dt))
+    HIPCALL(c, launch_cast_f32_half(c->dt, c->params, c->w_lp_flat, c->n_decay, s));
   if (c->n_flip) HIPCALL(c, launch_weight_flip_batched(c->dt, c->flip_jobs, c->n_flip, c->flip_total, s));
   return refresh_stem_pad(c, s);
 }
@@ -1096,18 +1102,22 @@ int refresh_compute_weights(seg_ctx* c, hipStream_t s) {
 extern "C" {
 
 const char* seg_last_error(seg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+int seg_set_loss_scale(seg_ctx* c, float scale);
 
 int seg_create(int device, const seg_cfg* cfg, seg_ctx** out) {
   if (!cfg || !out) return set_err(nullptr, -EINVAL, "null argument");
   *out = nullptr;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return set_err(nullptr, -ENODEV, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+  if (cfg->dtype < SEG_DTYPE_F32 || cfg->dtype > SEG_DTYPE_F16)
+    return set_err(nullptr, -EINVAL, "dtype %d (SEG_DTYPE_F32 / _BF16 / _F16)", cfg->dtype);
   seg_ctx* c = new seg_ctx();
   c->cfg = *cfg;
   c->device = device;
-  c->dt = cfg->dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32;
-  c->esz = c->dt == SEG_BF16 ? 2 : 4;
+  c->dt = dt_of(cfg->dtype);
+  c->esz = seg_half(c->dt) ? 2 : 4;
   int r = build(c);
+  if (!r && c->dt == SEG_F16) r = seg_set_loss_scale(c, 1.f);   // overflow flag of fp16 steps
   if (r) {
     std::string msg = c->err;
     seg_destroy(c);
@@ -1219,8 +1229,8 @@ int seg_loss(seg_ctx* c, const int32_t* px, const float* bbox, const float* tag,
   a.grad_un = c->grad_un; a.part = c->loss_part; a.decisions = decisions;
   hipStream_t s = (hipStream_t)stream;
   HIPCALL(c, launch_loss_head(a, c->tables, s));
-  HIPCALL(c, launch_loss_finalize(c->loss_part, c->loss_blocks, c->tables, c->ldl, c->loss_out,
-                                  c->dzscale, s));
+  HIPCALL(c, launch_loss_finalize(c->loss_part, c->loss_blocks, c->tables, c->ldl, c->loss_scale,
+                                  c->loss_out, c->dzscale, s));
   return 0;
 }
 
@@ -1234,12 +1244,19 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
                      void* stream) {
   NEED_BOUND(c);
   hipStream_t s = (hipStream_t)stream;
-  if (grad_scale != 1.f)
+  if (c->skip_flag) {   // loss-scaled (fp16) step: unscale, and skip it if anything overflowed
+    HIPCALL(c, hipMemsetAsync(c->skip_flag, 0, sizeof(int), s));
+    HIPCALL(c, launch_nonfinite(c->grads, c->n_train, c->skip_flag, s));
+    HIPCALL(c, launch_scale2(c->grads, c->n_train, grad_scale / c->loss_scale, c->n_stats, grad_scale, s));
+  } else if (grad_scale != 1.f) {
     HIPCALL(c, launch_scale_inplace(c->grads, c->n_train + c->n_stats, grad_scale, s));
+  }
   SgdmArgs a{};
   a.w = c->params; a.g = c->grads; a.v = c->mom;
   a.ema = ema_decay_eff > 0.f ? c->ema : nullptr;
-  a.w_lp = c->dt == SEG_BF16 ? (bf16_t*)c->w_lp_flat : nullptr;
+  a.w_lp = seg_half(c->dt) ? c->w_lp_flat : nullptr;
+  a.lp_f16 = c->dt == SEG_F16;
+  a.skip = c->skip_flag;
   a.n = c->n_decay; a.lr = lr; a.momentum = momentum; a.wd = c->cfg.weight_decay;
   a.ema_decay = ema_decay_eff; a.reg_part = c->reg_part;
   HIPCALL(c, launch_sgdm(a, s));
@@ -1276,6 +1293,21 @@ int seg_confusion(seg_ctx* c, const int32_t* labels, const int32_t* decisions, i
   hipError_t e = hipMemsetAsync(cm, 0, (size_t)num_classes * num_classes * 4, s);
   if (e == hipSuccess) e = launch_confusion(labels, decisions, n, num_classes, cm, s);
   if (e != hipSuccess) return hip_fail(c, e, "seg_confusion");
+  return 0;
+}
+
+int seg_set_loss_scale(seg_ctx* c, float scale) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (!(scale > 0.f)) return set_err(&c->err, -EINVAL, "loss scale must be > 0");
+  c->loss_scale = scale;
+  if (!c->skip_flag && (scale != 1.f || c->dt == SEG_F16))
+    if (int r = dalloc(c, &c->skip_flag, 1)) return r;
+  return 0;
+}
+
+int seg_found_inf(seg_ctx* c, const int32_t** flag) {
+  if (!c || !flag) return set_err(c ? &c->err : nullptr, -EINVAL, "null argument");
+  *flag = c->skip_flag;
   return 0;
 }
 
@@ -1320,7 +1352,7 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
   if (!c || !name) return set_err(c ? &c->err : nullptr, -EINVAL, "null argument");
   std::string n(name);
   Act a;
-  int dt = c->dt == SEG_BF16 ? SEG_DTYPE_BF16 : SEG_DTYPE_F32;
+  int dt = c->dt == SEG_BF16 ? SEG_DTYPE_BF16 : (c->dt == SEG_F16 ? SEG_DTYPE_F16 : SEG_DTYPE_F32);
   if (n == "logits") { a = c->logits; dt = SEG_DTYPE_F32; }
   else if (n == "grad_un") { a = c->logits; a.p = c->grad_un; dt = SEG_DTYPE_F32; }
   else if (n == "dzscale") { a.p = c->dzscale; a.N = a.H = a.W = 1; a.C = a.ld = c->ldl; dt = SEG_DTYPE_F32; }
@@ -1423,14 +1455,14 @@ int seg_op_conv_fwd(int dtype, const void* x, int N, int H, int W, int C, int ld
   a.x = x; a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx;
   a.w = w; a.ldw = k * k * C; a.y = y; a.Ho = Ho; a.Wo = Wo; a.Co = Co; a.ldy = ldy;
   a.KH = a.KW = k; a.sf = stride; a.st = 1; a.pad_h = ph; a.pad_w = pw; a.dil = rate; a.stats = stats;
-  hipError_t e = launch_conv_nt(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, 0, a, (hipStream_t)stream);
+  hipError_t e = launch_conv_nt(dt_of(dtype), 0, a, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_fwd");
 }
 
 int seg_op_conv_stat_rows(int dtype, int C, int ldx, int Co, int ldy, int k) {
   ConvArgs a{};
   a.C = C; a.ldx = ldx; a.Co = Co; a.ldy = ldy; a.ldw = 8; a.st = 1; a.KH = a.KW = k;
-  return conv_nt_stat_rows(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, 0, a);
+  return conv_nt_stat_rows(dt_of(dtype), 0, a);
 }
 
 int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
@@ -1445,7 +1477,7 @@ int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, 
   a.w = wt; a.ldw = k * k * Co; a.y = dx; a.Ho = H; a.Wo = W; a.Co = Ci; a.ldy = lddx;
   a.KH = a.KW = k; a.sf = 1; a.st = stride; a.pad_h = keff - 1 - ph; a.pad_w = keff - 1 - pw;
   a.dil = rate;
-  hipError_t e = launch_conv_nt(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, 0, a, (hipStream_t)stream);
+  hipError_t e = launch_conv_nt(dt_of(dtype), 0, a, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_dgrad");
 }
 
@@ -1465,7 +1497,7 @@ int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, 
   if ((int64_t)a.splits * n * 4 > ws_bytes) a.splits = (int)std::max<int64_t>(1, ws_bytes / (n * 4));
   a.out = (float*)workspace;
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = launch_conv_wgrad(dtype == SEG_DTYPE_BF16 ? SEG_BF16 : SEG_F32, a, s);
+  hipError_t e = launch_conv_wgrad(dt_of(dtype), a, s);
   if (e == hipSuccess) e = launch_splitk_reduce((float*)workspace, a.splits, n, n, dw, 0, s);
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_wgrad");
 }
@@ -1474,7 +1506,8 @@ int seg_op_conv_wgrad_cfg(int dtype, const void* dy, int N, int Ho, int Wo, int 
                           const void* x, int H, int W, int Ci, int ldx, int k, int stride, int rate,
                           int explicit_pad, float* dw, void* workspace, int64_t ws_bytes, int bm,
                           int bn, int splits, void* stream) {
-  if (dtype != SEG_DTYPE_BF16) return set_err(nullptr, -EINVAL, "wgrad_cfg: bf16 only");
+  if (dtype != SEG_DTYPE_BF16 && dtype != SEG_DTYPE_F16)
+    return set_err(nullptr, -EINVAL, "wgrad_cfg: 16-bit dtypes only");
   if ((bm != 64 && bm != 128 && bm != 256) || (bn != 64 && bn != 128 && bn != 256) || splits < 1)
     return set_err(nullptr, -EINVAL, "wgrad_cfg: tile must be 64/128/256, splits >= 1");
   int ho, wo, ph, pw;
@@ -1489,7 +1522,7 @@ int seg_op_conv_wgrad_cfg(int dtype, const void* dy, int N, int Ho, int Wo, int 
   if (!conv_wgrad_v2_ok(a)) return set_err(nullptr, -EINVAL, "wgrad_cfg: shape not on the v2 path");
   a.out = (float*)workspace;
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = launch_conv_wgrad_v2_tile(a, bm, bn, s);
+  hipError_t e = launch_conv_wgrad_v2_tile(dt_of(dtype), a, bm, bn, s);
   if (e == hipSuccess) e = launch_splitk_reduce((float*)workspace, splits, n, n, dw, 0, s);
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_wgrad_cfg");
 }

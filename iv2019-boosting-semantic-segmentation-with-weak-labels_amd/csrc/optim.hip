@@ -8,12 +8,14 @@ constexpr int SG_PER_BLOCK = SG_THREADS * 16;
 
 __global__ void sgdm_kernel(SgdmArgs a) {
   const long base = (long)blockIdx.x * SG_PER_BLOCK;
+  const bool skip = a.skip && *a.skip;   // dynamic loss scaling: overflowed step
   float reg = 0.f;
   for (int k = 0; k < 16; ++k) {
     const long i = base + (long)k * SG_THREADS + threadIdx.x;
     if (i >= a.n) break;
     const float w_old = a.w[i];
     reg += w_old * w_old;
+    if (skip) continue;
     // total gradient = d(seg)/dw + d(wd * sum(w^2)/2)/dw
     const float gt = a.g[i] + a.wd * w_old;
     // tf.train.MomentumOptimizer (use_nesterov=False): accum = accum*m + g; var -= lr*accum
@@ -22,7 +24,10 @@ __global__ void sgdm_kernel(SgdmArgs a) {
     const float w_new = w_old - a.lr * v;
     a.w[i] = w_new;
     if (a.ema) a.ema[i] -= (1.f - a.ema_decay) * (a.ema[i] - w_old);
-    if (a.w_lp) a.w_lp[i] = f2bf(w_new);
+    if (a.w_lp) {
+      if (a.lp_f16) ((f16_t*)a.w_lp)[i] = (f16_t)w_new;
+      else ((bf16_t*)a.w_lp)[i] = f2bf(w_new);
+    }
   }
   if (a.reg_part) {
     __shared__ float sh[SG_THREADS / 64];
@@ -53,6 +58,23 @@ __global__ void sum_partials_kernel(const float* __restrict__ p, int n, float* o
 __global__ void cast_kernel(const float* __restrict__ s, bf16_t* __restrict__ d, long n) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     d[i] = f2bf(s[i]);
+}
+
+__global__ void cast_f16_kernel(const float* __restrict__ s, f16_t* __restrict__ d, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    d[i] = (f16_t)s[i];
+}
+
+__global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* flag) {
+  bool bad = false;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) *flag = 1;
+}
+
+__global__ void scale2_kernel(float* x, long n1, float f1, long n2, float f2) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n1 + n2; i += (long)gridDim.x * blockDim.x)
+    x[i] *= i < n1 ? f1 : f2;
 }
 
 __global__ void scale_kernel(float* x, long n, float f) {
@@ -88,5 +110,27 @@ hipError_t launch_scale_inplace(float* x, long n, float f, hipStream_t s) {
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(scale_kernel, dim3((int)g), dim3(256), 0, s, x, n, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast_f32_half(int dtype, const float* src, void* dst, long n, hipStream_t s) {
+  if (dtype != SEG_F16) return launch_cast_f32_bf16(src, (bf16_t*)dst, n, s);
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(cast_f16_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, s, src, (f16_t*)dst, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_nonfinite(const float* x, long n, int* flag, hipStream_t s) {
+  long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, s, x, n, flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale2(float* x, long n1, float f1, long n2, float f2, hipStream_t s) {
+  long g = (n1 + n2 + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(scale2_kernel, dim3((int)(g < 1 ? 1 : g)), dim3(256), 0, s, x, n1, f1, n2, f2);
   return hipGetLastError();
 }

@@ -328,6 +328,9 @@ hipError_t launch_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, N, H, W, C,
                        ldx, (bf16_t*)y, Ho, Wo, ldy, pad_h, pad_w, (uint8_t*)arg);
+  else if (dtype == SEG_F16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<f16_t>, g, dim3(256), 0, s, (const f16_t*)x, N, H, W, C,
+                       ldx, (f16_t*)y, Ho, Wo, ldy, pad_h, pad_w, (uint8_t*)arg);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, dim3(256), 0, s, (const float*)x, N, H, W, C,
                        ldx, (float*)y, Ho, Wo, ldy, pad_h, pad_w, (uint8_t*)arg);
@@ -342,6 +345,9 @@ hipError_t launch_maxpool_bwd(int dtype, const void* arg, int N, int H, int W, i
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, N, H, W,
                        C, (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, pad_h, pad_w);
+  else if (dtype == SEG_F16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<f16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, N, H, W,
+                       C, (const f16_t*)dy, Ho, Wo, lddy, (f16_t*)dx, lddx, pad_h, pad_w);
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, dim3(256), 0, s, (const uint8_t*)arg, N, H, W,
                        C, (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, pad_h, pad_w);
@@ -355,6 +361,9 @@ hipError_t launch_add_strided(int dtype, void* dx, int H, int W, int lddx, const
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(add_strided_kernel<bf16_t>, gr, dim3(256), 0, s, (bf16_t*)dx, H, W, lddx,
                        (const bf16_t*)g, N, Ho, Wo, C, ldg, stride);
+  else if (dtype == SEG_F16)
+    hipLaunchKernelGGL(add_strided_kernel<f16_t>, gr, dim3(256), 0, s, (f16_t*)dx, H, W, lddx,
+                       (const f16_t*)g, N, Ho, Wo, C, ldg, stride);
   else
     hipLaunchKernelGGL(add_strided_kernel<float>, gr, dim3(256), 0, s, (float*)dx, H, W, lddx,
                        (const float*)g, N, Ho, Wo, C, ldg, stride);
@@ -369,12 +378,17 @@ hipError_t launch_grid_rowreduce(int dtype, const void* x, int N, int H, int W, 
   if (v8) {
     if (dtype == SEG_BF16)
       hipLaunchKernelGGL((grid_rowreduce8_kernel<bf16_t>), gr, dim3(256), 0, s, (const bf16_t*)x, N, H, W, C, ldx, g, part);
+    else if (dtype == SEG_F16)
+      hipLaunchKernelGGL((grid_rowreduce8_kernel<f16_t>), gr, dim3(256), 0, s, (const f16_t*)x, N, H, W, C, ldx, g, part);
     else
       hipLaunchKernelGGL((grid_rowreduce8_kernel<float>), gr, dim3(256), 0, s, (const float*)x, N, H, W, C, ldx, g, part);
     return hipGetLastError();
   }
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(grid_rowreduce_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)x, N, H,
+                       W, C, ldx, g, part);
+  else if (dtype == SEG_F16)
+    hipLaunchKernelGGL(grid_rowreduce_kernel<f16_t>, gr, dim3(256), 0, s, (const f16_t*)x, N, H,
                        W, C, ldx, g, part);
   else
     hipLaunchKernelGGL(grid_rowreduce_kernel<float>, gr, dim3(256), 0, s, (const float*)x, N, H, W,
@@ -392,6 +406,8 @@ hipError_t launch_grid_colreduce(int dtype, const float* part, int N, int H, int
   dim3 gr(ceil_div(total, 256));
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(grid_colreduce_kernel<bf16_t>, gr, dim3(256), 0, s, part, N, H, C, g, o);
+  else if (dtype == SEG_F16)
+    hipLaunchKernelGGL(grid_colreduce_kernel<f16_t>, gr, dim3(256), 0, s, part, N, H, C, g, o);
   else
     hipLaunchKernelGGL(grid_colreduce_kernel<float>, gr, dim3(256), 0, s, part, N, H, C, g, o);
   return hipGetLastError();
@@ -404,6 +420,9 @@ hipError_t launch_resize_fwd(int dtype, const void* x, int N, int hi, int wi, in
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(resize_fwd_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)x, N, hi, wi,
                        C, ldx, (bf16_t*)y, Ho, Wo, ldy);
+  else if (dtype == SEG_F16)
+    hipLaunchKernelGGL(resize_fwd_kernel<f16_t>, gr, dim3(256), 0, s, (const f16_t*)x, N, hi, wi,
+                       C, ldx, (f16_t*)y, Ho, Wo, ldy);
   else
     hipLaunchKernelGGL(resize_fwd_kernel<float>, gr, dim3(256), 0, s, (const float*)x, N, hi, wi, C,
                        ldx, (float*)y, Ho, Wo, ldy);
@@ -420,6 +439,9 @@ hipError_t launch_psp_input_bwd(int dtype, const void* dcat, int ldcat, const Gr
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(psp_input_bwd_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)dcat, ldcat,
                        g, ip, N, H, W, C, (bf16_t*)dx, lddx);
+  else if (dtype == SEG_F16)
+    hipLaunchKernelGGL(psp_input_bwd_kernel<f16_t>, gr, dim3(256), 0, s, (const f16_t*)dcat, ldcat,
+                       g, ip, N, H, W, C, (f16_t*)dx, lddx);
   else
     hipLaunchKernelGGL(psp_input_bwd_kernel<float>, gr, dim3(256), 0, s, (const float*)dcat, ldcat, g,
                        ip, N, H, W, C, (float*)dx, lddx);

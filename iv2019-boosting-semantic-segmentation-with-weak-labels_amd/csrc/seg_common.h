@@ -15,7 +15,13 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-enum SegDType { SEG_F32 = 0, SEG_BF16 = 1 };
+typedef _Float16 f16_t;   // storage type of fp16 activations/weights (BASELINE config C5)
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+
+enum SegDType { SEG_F32 = 0, SEG_BF16 = 1, SEG_F16 = 2 };
+// 16-bit storage (bf16 or fp16): the same kernels, data movement and fp32 accumulation; only
+// the MFMA opcode and the element conversions differ
+static inline bool seg_half(int dt) { return dt == SEG_BF16 || dt == SEG_F16; }
 
 // ---- scalar conversions ------------------------------------------------------------
 __device__ __host__ __forceinline__ float bf2f(bf16_t v) {
@@ -40,6 +46,10 @@ template <> struct TypeOps<float> {
 template <> struct TypeOps<bf16_t> {
   static __device__ __forceinline__ float to_f(bf16_t v) { return bf2f(v); }
   static __device__ __forceinline__ bf16_t from_f(float v) { return f2bf(v); }
+};
+template <> struct TypeOps<f16_t> {
+  static __device__ __forceinline__ float to_f(f16_t v) { return (float)v; }
+  static __device__ __forceinline__ f16_t from_f(float v) { return (f16_t)v; }   // RNE
 };
 template <typename T> __device__ __forceinline__ float ldf(const T* p) { return TypeOps<T>::to_f(*p); }
 template <typename T> __device__ __forceinline__ void stf(T* p, float v) { *p = TypeOps<T>::from_f(v); }
@@ -71,6 +81,47 @@ template <> struct Vec8<bf16_t> {
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
     *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
+template <> struct Vec8<f16_t> {
+  static __device__ __forceinline__ void load(const f16_t* p, float* o) {
+    const f16x8_t v = *(const f16x8_t*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+  }
+  static __device__ __forceinline__ void store(f16_t* p, const float* v) {
+    f16x8_t h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (f16_t)v[i];
+    *(f16x8_t*)p = h;
+  }
+};
+
+// 16-bit element traits of the MFMA kernels: fragment vector type, the 16x16x32 MFMA, and
+// the unpack of a raw 16-byte chunk
+template <typename E> struct Half;
+template <> struct Half<bf16_t> {
+  typedef bf16x8_t V;
+  static __device__ __forceinline__ f32x4_t mma(V a, V b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ void unpack(const uint4 u, float* o) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[2 * i] = bf2f((bf16_t)(w[i] & 0xffff)); o[2 * i + 1] = bf2f((bf16_t)(w[i] >> 16)); }
+  }
+};
+template <> struct Half<f16_t> {
+  typedef f16x8_t V;
+  static __device__ __forceinline__ f32x4_t mma(V a, V b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ void unpack(const uint4 u, float* o) {
+    f16x8_t h;
+    __builtin_memcpy(&h, &u, 16);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)h[i];
   }
 };
 

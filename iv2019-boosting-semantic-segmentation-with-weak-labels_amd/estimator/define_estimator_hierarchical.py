@@ -19,7 +19,7 @@ from __future__ import annotations
 from collections import namedtuple
 
 from estimator.define_losses_hierarchical import define_losses
-from estimator.define_optimizer import define_optimizer
+from estimator.define_optimizer import DynamicLossScaler, define_optimizer
 from estimator.mode_keys import ModeKeys
 
 EstimatorSpec = namedtuple('EstimatorSpec', ['mode', 'predictions', 'loss', 'train_op', 'losses'])
@@ -91,9 +91,13 @@ def define_estimator(mode, features, labels, model_fn, config, params):
     if mode != ModeKeys.TRAIN:
         raise NotImplementedError('EVAL/PREDICT are out of scope of the native training path')
     global_step = get_or_create_global_step()
+    ctx = predictions['_context']
+    # fp16 storage: dynamic loss scaling (the scale must be set before the loss seeds the
+    # backward); bf16 / fp32 need none
+    if getattr(ctx, 'dtype', None) == 'fp16' and getattr(ctx, '_scaler', None) is None:
+        ctx._scaler = DynamicLossScaler(ctx)
     losses = define_losses(mode, predictions, labels, config, params)
     optimizer = define_optimizer(global_step, params)
-    ctx = predictions['_context']
 
     def train_op():
         ctx.backward()
@@ -101,6 +105,8 @@ def define_estimator(mode, features, labels, model_fn, config, params):
         ema = 0.0 if world_size() > 1 else ema_decay_effective(params.ema_decay, global_step.value)
         ctx.apply_update(optimizer.learning_rate(global_step.value), optimizer.momentum,
                          ema, scale)
+        if getattr(ctx, '_scaler', None) is not None:
+            ctx._scaler.update()   # an overflowed step was skipped on the device
         global_step.value += 1
         return losses
 

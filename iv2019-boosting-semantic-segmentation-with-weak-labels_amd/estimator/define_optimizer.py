@@ -56,3 +56,32 @@ def define_optimizer(global_step, params):
                      final=params.learning_rate_final, power=params.learning_rate_power,
                      decay_steps=max(int(getattr(params, 'num_training_steps', 1)), 1),
                      momentum=momentum, use_nesterov=False)
+
+
+class DynamicLossScaler:
+    """fp16 loss scaling (BASELINE config C5: fp16 storage with fp32 master gradients), the
+    usual dynamic policy: start at 2**16; a step whose loss-scaled gradients overflow is
+    skipped on the device (seg_apply_update) and halves the scale; `growth_interval` clean
+    steps double it. `update(ctx)` reads the device overflow flag of the step just issued."""
+
+    def __init__(self, ctx, init_scale=2.0 ** 16, growth_interval=2000, backoff=0.5, growth=2.0,
+                 min_scale=1.0):
+        self.ctx, self.scale, self.growth_interval = ctx, float(init_scale), growth_interval
+        self.backoff, self.growth, self.min_scale = backoff, growth, min_scale
+        self.good_steps, self.skipped, self.last_overflow = 0, 0, False
+        ctx.set_loss_scale(self.scale)
+
+    def update(self):
+        flag = self.ctx.found_inf()
+        overflow = bool(int(flag.item())) if flag is not None else False
+        self.last_overflow = overflow
+        if overflow:
+            self.skipped += 1
+            self.good_steps = 0
+            self.scale = max(self.scale * self.backoff, self.min_scale)
+        else:
+            self.good_steps += 1
+            if self.good_steps % self.growth_interval == 0:
+                self.scale *= self.growth
+        self.ctx.set_loss_scale(self.scale)
+        return overflow

@@ -117,5 +117,5 @@ def add_model_arguments(argparser):
     # ASPP: the reference's commented-out _create_aspp_module (hierarchical.py:209-226), built
     # in the PSP call site's 'pyramid_module' scope; mutually exclusive with --psp_module
     a('--aspp_module', action='store_true')
-    a('--compute_dtype', type=str, default='bf16', choices=['bf16', 'fp32'])
+    a('--compute_dtype', type=str, default='bf16', choices=['bf16', 'fp16', 'fp32'])
     a('--init_seed', type=int, default=0)

@@ -25,11 +25,11 @@ EXPORTED_SYMBOLS = [
     "seg_profile", "seg_profile_dump",
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
-    "seg_grad_buckets", "seg_stream_wait_bucket",
+    "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
 ]
 
 PYRAMID = {"none": 0, "psp": 1, "aspp": 2}
-DTYPE = {"fp32": 0, "bf16": 1}
+DTYPE = {"fp32": 0, "bf16": 1, "fp16": 2}
 DATASET = {"cityscapes": 0, "vistas": 1}
 PARAM_KIND = {0: "weights", 1: "gamma", 2: "beta", 3: "moving_mean", 4: "moving_variance"}
 
@@ -91,6 +91,8 @@ def _load():
         "seg_bbox_labels": (ip, [vp, vp, vp, vp, ip, ip, ip, ip, vp, vp]),
         "seg_grad_buckets": (ip, [vp, ip, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
         "seg_stream_wait_bucket": (ip, [vp, ip, vp]),
+        "seg_set_loss_scale": (ip, [vp, ctypes.c_float]),
+        "seg_found_inf": (ip, [vp, ctypes.POINTER(ctypes.c_void_p)]),
         "seg_tag_labels": (ip, [vp, ip, ip, ip, vp, vp]),
     }
     for name, (res, args) in sig.items():
@@ -216,6 +218,17 @@ class SegContext:
     def backward(self, stream=None):
         check(LIB.seg_backward(self.h, _stream(stream)), self.h)
 
+    def set_loss_scale(self, scale: float):
+        """Gradient-seed multiplier (fp16 dynamic loss scaling; see seg_set_loss_scale)."""
+        check(LIB.seg_set_loss_scale(self.h, float(scale)), self.h)
+        self.loss_scale = float(scale)
+
+    def found_inf(self):
+        """Device int32 view of the last update's overflow flag (None unless loss scaling)."""
+        p = ctypes.c_void_p()
+        check(LIB.seg_found_inf(self.h, ctypes.byref(p)), self.h)
+        return None if not p.value else _wrap_i32(p.value, (1,), self.device)
+
     def grad_buckets(self):
         """[(lo, hi)] ranges of self.grads in the order the backward completes them."""
         n = LIB.seg_grad_buckets(self.h, 0, None, None)
@@ -261,7 +274,7 @@ class SegContext:
         if dt.value == 0:
             t = _wrap(ptr.value, (n * hh * ww, ld.value), self.device)
         else:
-            t = _wrap_u16(ptr.value, (n * hh * ww, ld.value), self.device)
+            t = _wrap_u16(ptr.value, (n * hh * ww, ld.value), self.device, half=dt.value == 2)
         return t[:, :c].float().cpu().numpy().reshape(n, hh, ww, c)
 
     def profile(self, enable: bool):
@@ -300,8 +313,8 @@ class SegContext:
             pass
 
 
-def _wrap_u16(ptr: int, shape: Tuple[int, ...], device):
-    """Zero-copy view of a bf16 device buffer (reinterpreted from int16)."""
+def _wrap_u16(ptr: int, shape: Tuple[int, ...], device, half=False):
+    """Zero-copy view of a bf16 (or fp16) device buffer (reinterpreted from int16)."""
     import torch
 
     class _CAI:
@@ -309,7 +322,18 @@ def _wrap_u16(ptr: int, shape: Tuple[int, ...], device):
     o = _CAI()
     o.__cuda_array_interface__ = {"shape": shape, "typestr": "<i2", "data": (ptr, False),
                                   "version": 3, "strides": None}
-    return torch.as_tensor(o, device=device).view(torch.bfloat16)
+    return torch.as_tensor(o, device=device).view(torch.float16 if half else torch.bfloat16)
+
+
+def _wrap_i32(ptr: int, shape: Tuple[int, ...], device):
+    import torch
+
+    class _CAI:
+        pass
+    o = _CAI()
+    o.__cuda_array_interface__ = {"shape": shape, "typestr": "<i4", "data": (ptr, False),
+                                  "version": 3, "strides": None}
+    return torch.as_tensor(o, device=device)
 
 
 def _wrap(ptr: int, shape: Tuple[int, ...], device):

@@ -1,7 +1,7 @@
-"""Parity of the implicit-GEMM conv kernels (fwd / dgrad / wgrad, fp32 and bf16) against the
-oracle's TF-semantics conv (torch CPU, float64). Tolerances: fp32 rel 1e-4 (exact-fp32 MFMA
-with a different summation order), bf16 rel 2e-2 against a reference fed the same
-bf16-rounded operands (fp32 accumulation on both sides)."""
+"""Parity of the implicit-GEMM conv kernels (fwd / dgrad / wgrad, fp32, bf16 and fp16) against
+the oracle's TF-semantics conv (torch CPU, float64). Tolerances: fp32 rel 1e-4 (exact-fp32
+MFMA with a different summation order), bf16 rel 2e-2 and fp16 rel 3e-3 against a reference
+fed the same rounded operands (fp32 accumulation on both sides; the output is rounded once)."""
 import numpy as np
 import pytest
 import torch
@@ -41,6 +41,15 @@ def _bf16_round(a):
     return torch.as_tensor(a).to(torch.bfloat16).to(torch.float32).numpy()
 
 
+TDT = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
+ABI = {"fp32": 0, "bf16": 1, "fp16": 2}
+TOL = {"fp32": 1e-4, "bf16": 2e-2, "fp16": 3e-3}
+
+
+def _round(a, dtype):
+    return torch.as_tensor(a).to(TDT[dtype]).to(torch.float32).numpy()
+
+
 def _geom(case):
     N, H, W, Ci, Co, k, s, r, ep = case
     spec = ConvSpec("t", Ci, Co, k, s, r, explicit_pad=ep)
@@ -54,16 +63,16 @@ def _ref_conv(x, w, spec):
     return conv_tf(xt, torch.as_tensor(w, dtype=torch.float64), spec).permute(0, 2, 3, 1).numpy()
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", CASES)
 def test_conv_fwd(cuda, dtype, case):
     from seg_hip import LIB, check
     N, H, W, Ci, Co, k, s, r, ep = case
     x, w = _tensors(case)
     spec, Ho, Wo = _geom(case)
-    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
-    if dtype == "bf16":
-        x, w = _bf16_round(x), _bf16_round(w)
+    tdt = TDT[dtype]
+    if dtype != "fp32":
+        x, w = _round(x, dtype), _round(w, dtype)
     ref = _ref_conv(x, w, spec)
     xd = torch.as_tensor(x).to(cuda, tdt).contiguous()
     wd = torch.as_tensor(w).to(cuda, tdt).contiguous()
@@ -71,15 +80,15 @@ def test_conv_fwd(cuda, dtype, case):
     M = N * Ho * Wo
     stats = torch.zeros(((M + 127) // 128, Co, 2), dtype=torch.float32, device=cuda)
     s_ = torch.cuda.current_stream().cuda_stream
-    check(LIB.seg_op_conv_fwd(1 if dtype == "bf16" else 0, xd.data_ptr(), N, H, W, Ci, Ci,
+    check(LIB.seg_op_conv_fwd(ABI[dtype], xd.data_ptr(), N, H, W, Ci, Ci,
                               wd.data_ptr(), Co, k, s, r, int(ep), yd.data_ptr(), Co,
                               stats.data_ptr(), s_))
     torch.cuda.synchronize()
     y = yd.float().cpu().numpy()
-    tol = 1e-4 if dtype == "fp32" else 2e-2
+    tol = TOL[dtype]
     assert _rel(y, ref) < tol
     # BN partial statistics: merge (sum, M2 about the tile mean) and compare
-    tr = LIB.seg_op_conv_stat_rows(1 if dtype == "bf16" else 0, Ci, Ci, Co, Co, k)
+    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], Ci, Ci, Co, Co, k)
     nt = (M + tr - 1) // tr
     st = stats.cpu().numpy().astype(np.float64)[:nt]
     cnt = np.minimum(tr, M - np.arange(nt) * tr).astype(np.float64)
@@ -95,7 +104,7 @@ def test_conv_fwd(cuda, dtype, case):
     assert _rel(m2 / M, yr.var(0)) < 1e-3
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", [c for c in CASES if c[3] != 3])
 def test_conv_dgrad(cuda, dtype, case):
     from seg_hip import LIB, check
@@ -103,9 +112,9 @@ def test_conv_dgrad(cuda, dtype, case):
     x, w = _tensors(case)
     spec, Ho, Wo = _geom(case)
     g = np.random.default_rng(1).standard_normal((N, Ho, Wo, Co)).astype(np.float32)
-    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
-    if dtype == "bf16":
-        w, g = _bf16_round(w), _bf16_round(g)
+    tdt = TDT[dtype]
+    if dtype != "fp32":
+        w, g = _round(w, dtype), _round(g, dtype)
     xt = torch.as_tensor(x, dtype=torch.float64).permute(0, 3, 1, 2).requires_grad_(True)
     y = conv_tf(xt, torch.as_tensor(w, dtype=torch.float64), spec)
     y.backward(torch.as_tensor(g, dtype=torch.float64).permute(0, 3, 1, 2))
@@ -114,15 +123,14 @@ def test_conv_dgrad(cuda, dtype, case):
     gd = torch.as_tensor(g).to(cuda, tdt).contiguous()
     wtd = torch.as_tensor(wt).to(cuda, tdt).contiguous()
     dx = torch.zeros((N, H, W, Ci), dtype=tdt, device=cuda)
-    check(LIB.seg_op_conv_dgrad(1 if dtype == "bf16" else 0, gd.data_ptr(), N, Ho, Wo, Co, Co,
+    check(LIB.seg_op_conv_dgrad(ABI[dtype], gd.data_ptr(), N, Ho, Wo, Co, Co,
                                 wtd.data_ptr(), Ci, k, s, r, int(ep), H, W, dx.data_ptr(), Ci,
                                 torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
-    tol = 1e-4 if dtype == "fp32" else 2e-2
-    assert _rel(dx.float().cpu().numpy(), ref) < tol
+    assert _rel(dx.float().cpu().numpy(), ref) < TOL[dtype]
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", CASES)
 def test_conv_wgrad(cuda, dtype, case):
     from seg_hip import LIB, check
@@ -132,9 +140,9 @@ def test_conv_wgrad(cuda, dtype, case):
     x, w = _tensors(case)
     spec, Ho, Wo = _geom(case)
     g = np.random.default_rng(2).standard_normal((N, Ho, Wo, Co)).astype(np.float32)
-    tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
-    if dtype == "bf16":
-        x, g = _bf16_round(x), _bf16_round(g)
+    tdt = TDT[dtype]
+    if dtype != "fp32":
+        x, g = _round(x, dtype), _round(g, dtype)
     wt = torch.as_tensor(w, dtype=torch.float64).requires_grad_(True)
     y = conv_tf(torch.as_tensor(x, dtype=torch.float64).permute(0, 3, 1, 2), wt, spec)
     y.backward(torch.as_tensor(g, dtype=torch.float64).permute(0, 3, 1, 2))
@@ -143,12 +151,11 @@ def test_conv_wgrad(cuda, dtype, case):
     gd = torch.as_tensor(g).to(cuda, tdt).contiguous()
     dw = torch.zeros((Co, k, k, Ci), dtype=torch.float32, device=cuda)
     ws = torch.zeros(64 << 20, dtype=torch.uint8, device=cuda)
-    check(LIB.seg_op_conv_wgrad(1 if dtype == "bf16" else 0, gd.data_ptr(), N, Ho, Wo, Co, Co,
+    check(LIB.seg_op_conv_wgrad(ABI[dtype], gd.data_ptr(), N, Ho, Wo, Co, Co,
                                 xd.data_ptr(), H, W, Ci, Ci, k, s, r, int(ep), dw.data_ptr(),
                                 ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
-    tol = 1e-4 if dtype == "fp32" else 2e-2
-    assert _rel(dw.cpu().numpy(), ref) < tol
+    assert _rel(dw.cpu().numpy(), ref) < TOL[dtype]
 
 
 WGRAD_CFG_CASES = [
@@ -163,27 +170,28 @@ WGRAD_CFG_CASES = [
 ]
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("case,bm,bn,splits", WGRAD_CFG_CASES)
-def test_conv_wgrad_cfg(cuda, case, bm, bn, splits):
+def test_conv_wgrad_cfg(cuda, case, bm, bn, splits, dtype):
     """bf16 weight gradient at an explicit tile / split configuration (every kernel the
     runtime can pick, reached at test sizes), vs float64 on the same bf16 operands."""
     from seg_hip import LIB, check
     N, H, W, Ci, Co, k, s, r, ep = case
     x, w = _tensors(case)
     spec, Ho, Wo = _geom(case)
-    g = _bf16_round(np.random.default_rng(3).standard_normal((N, Ho, Wo, Co)).astype(np.float32))
-    x = _bf16_round(x)
+    g = _round(np.random.default_rng(3).standard_normal((N, Ho, Wo, Co)).astype(np.float32), dtype)
+    x = _round(x, dtype)
     wt = torch.as_tensor(w, dtype=torch.float64).requires_grad_(True)
     y = conv_tf(torch.as_tensor(x, dtype=torch.float64).permute(0, 3, 1, 2), wt, spec)
     y.backward(torch.as_tensor(g, dtype=torch.float64).permute(0, 3, 1, 2))
     ref = wt.grad.numpy()
-    xd = torch.as_tensor(x).to(cuda, torch.bfloat16).contiguous()
-    gd = torch.as_tensor(g).to(cuda, torch.bfloat16).contiguous()
+    xd = torch.as_tensor(x).to(cuda, TDT[dtype]).contiguous()
+    gd = torch.as_tensor(g).to(cuda, TDT[dtype]).contiguous()
     dw = torch.zeros((Co, k, k, Ci), dtype=torch.float32, device=cuda)
     ws = torch.full((splits * Co * k * k * Ci,), float("nan"), dtype=torch.float32, device=cuda)
-    check(LIB.seg_op_conv_wgrad_cfg(1, gd.data_ptr(), N, Ho, Wo, Co, Co, xd.data_ptr(), H, W, Ci,
+    check(LIB.seg_op_conv_wgrad_cfg(ABI[dtype], gd.data_ptr(), N, Ho, Wo, Co, Co, xd.data_ptr(), H, W, Ci,
                                     Ci, k, s, r, int(ep), dw.data_ptr(), ws.data_ptr(),
                                     ws.numel() * 4, bm, bn, splits,
                                     torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
-    assert _rel(dw.cpu().numpy(), ref) < 2e-2
+    assert _rel(dw.cpu().numpy(), ref) < TOL[dtype]

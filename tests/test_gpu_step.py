@@ -21,6 +21,8 @@ from oracle.tfseg import OracleNet, SegConfig, init_params
 
 pytestmark = pytest.mark.gpu
 
+HALF = {"bf16": torch.bfloat16, "fp16": torch.float16}
+
 
 def _rel(a, b):
     a = np.asarray(a, np.float64)
@@ -120,8 +122,9 @@ def test_train_step_fp32(cuda, cfg):
             assert _rel(nat["params"][k], v.detach().numpy().reshape(-1)) < 1e-3, k
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("pyramid", ["psp", "aspp"])
-def test_bf16_layerwise(cuda, pyramid):
+def test_bf16_layerwise(cuda, pyramid, dtype):
     """bf16 storage / fp32 accumulation, layer by layer.
 
     End-to-end bf16-vs-fp64 comparison is meaningless at random init: the network is chaotic
@@ -134,7 +137,7 @@ def test_bf16_layerwise(cuda, pyramid):
     cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid=pyramid)
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=5).items()}
     data = batch(12, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
-    ctx = SegContext(pyramid=pyramid, height=64, width=128, nb_pp=1, nb_pb=1, dtype="bf16")
+    ctx = SegContext(pyramid=pyramid, height=64, width=128, nb_pp=1, nb_pb=1, dtype=dtype)
     ctx.load_params(params)
     ctx.forward(torch.as_tensor(data["images"]).to(cuda))
     ctx.loss(torch.as_tensor(data["px"]).to(cuda), torch.as_tensor(data["bbox"]).to(cuda))
@@ -143,10 +146,10 @@ def test_bf16_layerwise(cuda, pyramid):
     assert np.all(np.isfinite(lv)) and 0.5 < lv[1] < 10.0
     for i, s in enumerate(build_specs(cfg)):
         x = torch.as_tensor(ctx.debug_tensor(f"conv{i}_x"), dtype=torch.float64).permute(0, 3, 1, 2)
-        w = torch.as_tensor(params[s.name + "/weights"]).to(torch.bfloat16).double()
+        w = torch.as_tensor(params[s.name + "/weights"]).to(HALF[dtype]).double()
         ref = conv_tf(x, w, s).permute(0, 2, 3, 1).numpy()
         y = ctx.debug_tensor(f"conv{i}_y")
-        assert _rel(y, ref) < 1e-2, (s.name, _rel(y, ref))
+        assert _rel(y, ref) < (1e-2 if dtype == "bf16" else 2e-3), (s.name, _rel(y, ref))
     ctx.close()
 
 
@@ -221,7 +224,8 @@ def _bn_bwd_ref(dz, y, z, gamma, eps=1.001e-5):
     return dy.reshape(y.shape)
 
 
-def test_bf16_backward_layerwise(cuda):
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_bf16_backward_layerwise(cuda, dtype):
     """bf16 backward, unit by unit, on the tensors the native step itself produced: for each
     bottleneck, the data gradient of conv3 / conv2 (v2 dgrad) feeding the fused ReLU-mask +
     BN-backward epilogue must give conv2 / conv1's dy, and every conv's weight gradient must
@@ -233,8 +237,10 @@ def test_bf16_backward_layerwise(cuda):
     cfg = SegConfig(height=64, width=128, nb_pp=2, pyramid="psp")
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=7).items()}
     data = batch(13, cfg.nb_pp, 0, 0, cfg.height, cfg.width)
-    ctx = SegContext(pyramid="psp", height=64, width=128, nb_pp=2, dtype="bf16")
+    ctx = SegContext(pyramid="psp", height=64, width=128, nb_pp=2, dtype=dtype)
     ctx.load_params(params)
+    if dtype == "fp16":
+        ctx.set_loss_scale(1024.0)   # keeps the fp16 gradients in the normal range
     ctx.forward(torch.as_tensor(data["images"]).to(cuda))
     ctx.loss(torch.as_tensor(data["px"]).to(cuda))
     ctx.backward()
@@ -243,7 +249,7 @@ def test_bf16_backward_layerwise(cuda):
     specs = build_specs(cfg)
     idx = {s.name: i for i, s in enumerate(specs)}
     T = lambda a: torch.as_tensor(a, dtype=torch.float64).permute(0, 3, 1, 2)
-    wbf = lambda n: torch.as_tensor(params[n + "/weights"]).to(torch.bfloat16).double()
+    wbf = lambda n: torch.as_tensor(params[n + "/weights"]).to(HALF[dtype]).double()
     checked = 0
     for s in specs:
         unit = s.name[:-len("/conv1")]
@@ -276,4 +282,45 @@ def test_bf16_backward_layerwise(cuda):
     conv_tf(T(ctx.debug_tensor("conv0_x")), w, sp).backward(T(ctx.debug_tensor("conv0_dy")))
     ref = w.grad.numpy().reshape(-1)
     assert _rel(grads[sp.name + "/weights"], ref) < 2e-2, _rel(grads[sp.name + "/weights"], ref)
+    ctx.close()
+
+
+def test_fp16_loss_scaling_unscales_and_skips_overflow(cuda):
+    """fp16 storage with fp32 master weights (BASELINE config C5): the loss scale multiplies
+    the gradient seed and seg_apply_update divides it back out of the weight / BN gradients
+    (not the batch-statistics tail); a scale that overflows the fp16 backward flags the step
+    and leaves every parameter untouched."""
+    from input_pipelines.synthetic import batch
+    from seg_hip import SegContext
+    cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="psp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=5).items()}
+    data = batch(12, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
+    img = torch.as_tensor(data["images"]).to(cuda)
+    px, bb = torch.as_tensor(data["px"]).to(cuda), torch.as_tensor(data["bbox"]).to(cuda)
+    ctx = SegContext(pyramid="psp", height=64, width=128, nb_pp=1, nb_pb=1, dtype="fp16")
+    ctx.load_params(params)
+
+    def step(scale, lr):
+        ctx.load_params(params)
+        ctx.set_loss_scale(scale)
+        ctx.forward(img)
+        ctx.loss(px, bb)
+        ctx.backward()
+        ctx.apply_update(lr, 0.9)
+        torch.cuda.synchronize()
+        return ctx.grads.cpu().clone(), ctx.params.cpu().clone(), int(ctx.found_inf().item())
+    g1, p1, f1 = step(256.0, 0.0)
+    g2, p2, f2 = step(4096.0, 0.0)
+    assert f1 == 0 and f2 == 0
+    n = ctx.params.numel()
+    # unscaled weight gradients agree across scales (fp16 rounding of the scaled backward)
+    assert _rel(g1[:n].numpy(), g2[:n].numpy()) < 2e-2
+    # the batch-statistics tail is not divided by the loss scale
+    assert torch.equal(g1[n:], g2[n:])
+    # overflow: every parameter kept, flag raised
+    ctx.load_params(params)
+    p0 = ctx.params.cpu().clone()
+    g3, p3, f3 = step(1e38, 0.01)
+    assert f3 == 1
+    assert torch.equal(p3, p0)
     ctx.close()
