@@ -159,18 +159,6 @@ def main():
         elapsed = float(t.item())
     losses, _, _ = ctx.outputs()
     lv = losses.cpu().numpy()
-    # training-summary mIoU of the metric (define_metrics.py:5-20 via the device confusion
-    # kernel), on the strong images of one extra forward + loss with fused decisions, outside
-    # the timed region; random-init weights, so it only exercises the path (the reference's
-    # 70.46 needs trained weights and Cityscapes, neither available here)
-    miou = None
-    if nb_pp:
-        from estimator.define_metrics import confusion_matrix, mean_iou_from_cm
-        dec = torch.empty((nb_pp + nb_pb + nb_pi, H, W), dtype=torch.int32, device=dev)
-        ctx.forward(img)
-        ctx.loss(px, bbox, tag, dec)
-        cm = confusion_matrix(ctx, px, dec[:nb_pp], 20)
-        miou = round(float(mean_iou_from_cm(cm)), 5)
     if not np.all(np.isfinite(lv)):
         raise RuntimeError(f"non-finite losses {lv}")
 
@@ -239,6 +227,18 @@ def main():
                     "max_layer": r["max_layer"]}
         ctx.profile(False)
 
+    # training-summary mIoU of the metric (define_metrics.py:5-20 via the device confusion
+    # kernel), on the strong images of one extra forward + loss with fused decisions, outside
+    # the timed region and after the profiled step has been read; random-init weights, so it
+    # only exercises the path (the reference's 70.46 needs trained weights and Cityscapes)
+    miou = None
+    if nb_pp:
+        from estimator.define_metrics import confusion_matrix, mean_iou_from_cm
+        dec = torch.empty((nb_pp + nb_pb + nb_pi, H, W), dtype=torch.int32, device=dev)
+        ctx.forward(img)
+        ctx.loss(px, bbox, tag, dec)
+        cm = confusion_matrix(ctx, px, dec[:nb_pp], 20)
+        miou = round(float(mean_iou_from_cm(cm)), 5)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C2":
         cpu = cpu_baseline(threads=min(16, os.cpu_count() or 1), pyramid=args.pyramid)

@@ -82,6 +82,8 @@ int seg_param_shape(seg_ctx* ctx, int64_t i, int64_t* dims);
 int seg_params_updated(seg_ctx* ctx, void* stream);
 
 /* one training step -------------------------------------------------------------------- */
+/* images_nhwc [N][H][W][3] fp32 is read (copied / converted into the context) on `stream`;
+ * the caller's buffer may be released once the forward's work on that stream is done */
 int seg_forward(seg_ctx* ctx, const float* images_nhwc, void* stream);
 int seg_loss(seg_ctx* ctx, const int32_t* px_labels, const float* bbox_soft,
              const float* tag_soft, int32_t* decisions_out, void* stream);
@@ -107,6 +109,19 @@ int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions,
  * The caller adjusts the scale from the flag (dynamic loss scaling). */
 int seg_set_loss_scale(seg_ctx* ctx, float scale);
 int seg_found_inf(seg_ctx* ctx, const int32_t** flag_device);
+
+/* cross-replica (synchronised) batch norm, the reference's --cross_replica_norm
+ * (models/resnet50_extended_model_hierarchical.py:327-328 -> utils/cross_replica_batch_
+ * normalization.py:393-476). With a hook set, every BN layer of seg_forward exchanges its
+ * per-channel [mean | E[x^2]] (2C floats) and normalises with the replica average: mean,
+ * variance E[x^2] - mean^2 (biased; it also feeds the moving variance, as the reference's
+ * non-fused path does); every BN layer of seg_backward exchanges [mean(dyhat) |
+ * mean(dyhat * xhat)] so dx is the gradient through the global statistics. `allreduce` must
+ * SUM `n` floats at the device pointer `buf` in place across the `world` replicas, ordered
+ * on `stream` (e.g. torch.distributed.all_reduce on that stream, RCCL or gloo), and return 0;
+ * a nonzero return fails the step. fn = NULL (or world = 1) turns synchronisation off. */
+typedef int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, hipStream_t stream);
+int seg_set_bn_sync(seg_ctx* ctx, seg_allreduce_fn allreduce, void* user, int world);
 
 /* gradient all-reduce buckets, in the order the backward completes them: n buckets
  * [lo[i], hi[i]) of the flat [grads | BN stats] buffer (conv-weight ranges cut at layer

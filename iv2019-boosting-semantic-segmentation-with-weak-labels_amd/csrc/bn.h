@@ -46,9 +46,13 @@ struct BnBwdArgs {
   int rb;                          // number of row blocks
 };
 
+// pack (nullable, [2C]): also writes [mean | E[x^2]] for a cross-replica exchange
 hipError_t launch_bn_stats_finalize(const float* tile_part, long M, int C, int tile_rows,
                                     float* scratch, const float* gamma, BnState st,
-                                    hipStream_t s);
+                                    hipStream_t s, float* pack = nullptr);
+// cross-replica BN: the replica-summed pack -> global mean / biased variance in st
+hipError_t launch_bn_sync_unpack(const float* pack, int C, float inv_world, const float* gamma,
+                                 BnState st, hipStream_t s);
 hipError_t launch_bn_apply(int dtype, int out_f32, const BnApplyArgs& a, hipStream_t s);
 int bn_bwd_rowblocks(long M, int C);
 hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipStream_t s);

@@ -47,7 +47,7 @@ __global__ void bn_stats_stage1(const float* __restrict__ part, long M, int C, i
 }
 
 __global__ void bn_stats_stage2(const float* __restrict__ g, int G, int C, const float* gamma,
-                                BnState st) {
+                                BnState st, float* pack) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float n = 0.f, mean = 0.f, m2 = 0.f;
@@ -61,6 +61,26 @@ __global__ void bn_stats_stage2(const float* __restrict__ g, int G, int C, const
   st.invstd[c] = inv;
   st.scale[c] = gamma[c] * inv;
   st.var_unb[c] = m2 / (n > 1.f ? n - 1.f : 1.f);
+  if (pack) {   // this replica's moments for the cross-replica exchange
+    pack[c] = mean;
+    pack[C + c] = var + mean * mean;
+  }
+}
+
+// cross_replica_batch_normalization.py:400-425: global mean = mean of the replica means,
+// global variance = mean of the replica E[x^2] - mean^2 (no Bessel factor: the non-fused
+// path's variance also feeds the moving average, :452-466 with _bessels_correction_test_only)
+__global__ void bn_sync_unpack_kernel(const float* __restrict__ pack, int C, float inv_world,
+                                      const float* gamma, BnState st) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float mean = pack[c] * inv_world;
+  const float var = pack[C + c] * inv_world - mean * mean;
+  const float inv = rsqrtf(var + SEG_BN_EPS);
+  st.mean[c] = mean;
+  st.invstd[c] = inv;
+  st.scale[c] = gamma[c] * inv;
+  st.var_unb[c] = var;
 }
 
 // ---- forward apply ---------------------------------------------------------------------
@@ -629,13 +649,20 @@ hipError_t bwd_apply_t(const BnBwdArgs& a, hipStream_t s) {
 
 hipError_t launch_bn_stats_finalize(const float* tile_part, long M, int C, int tile_rows,
                                     float* scratch, const float* gamma, BnState st,
-                                    hipStream_t s) {
+                                    hipStream_t s, float* pack) {
   int ntiles = ceil_div(M, tile_rows);
   int G = ceil_div(ntiles, STAT_TPB);
   hipLaunchKernelGGL(bn_stats_stage1, dim3(ceil_div(C, 64), G), dim3(256), 0, s, tile_part, M, C,
                      tile_rows, ntiles, scratch);
   hipLaunchKernelGGL(bn_stats_stage2, dim3(ceil_div(C, 64)), dim3(64), 0, s, scratch, G, C, gamma,
-                     st);
+                     st, pack);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_sync_unpack(const float* pack, int C, float inv_world, const float* gamma,
+                                 BnState st, hipStream_t s) {
+  hipLaunchKernelGGL(bn_sync_unpack_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, s, pack, C,
+                     inv_world, gamma, st);
   return hipGetLastError();
 }
 

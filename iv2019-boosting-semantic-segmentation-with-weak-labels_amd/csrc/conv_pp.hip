@@ -464,9 +464,15 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
       if (nres) bf8_add(v, r1v[rr]);
       if (nres == 2) bf8_add(v, r2v[rr]);
+#ifdef PP_DBG_NOSTORE
+      if (v[0] == 1234.5f)
+#endif
       if (n < a.Co && m < M) Vec8<E>::store(Y + (size_t)m * a.ldy + n, v);
     }
     epi_sync();
+#ifdef PP_DBG_NOSTAGE
+    break;
+#endif
   }
   if (!has_next) break;
   tile = tile_n;

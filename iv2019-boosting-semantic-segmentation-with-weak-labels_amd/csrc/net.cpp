@@ -154,6 +154,11 @@ struct seg_ctx {
   int bk_next = 0;
   // backward on two streams: every weight gradient runs on `side` (waiting for its layer's
   // dy on the compute stream), so the dgrad -> BN-backward chain and the wgrads overlap
+  // cross-replica BN (seg_set_bn_sync): per-layer moment exchange through the caller's hook
+  seg_allreduce_fn sync_fn = nullptr;
+  void* sync_user = nullptr;
+  int sync_world = 1;
+  float* sync_pack = nullptr;     // [2 * max C]
   float loss_scale = 1.f;         // gradient seed multiplier (fp16 dynamic loss scaling)
   int* skip_flag = nullptr;       // device: non-finite scaled gradients this step (update skipped)
   bool side_on = false;
@@ -403,6 +408,13 @@ int prof_end(seg_ctx* c, hipStream_t s, int slot) {
   return 0;
 }
 
+// one cross-replica exchange (SUM in place, ordered on stream s) through the caller's hook
+int sync_exchange(seg_ctx* c, float* buf, long n, hipStream_t s) {
+  const int r = c->sync_fn(c->sync_user, buf, (int64_t)n, s);
+  if (r) return set_err(&c->err, -EIO, "cross-replica BN exchange failed (hook returned %d)", r);
+  return 0;
+}
+
 int conv_forward(Step& S, int li, const Act& x) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
@@ -421,8 +433,14 @@ int conv_forward(Step& S, int li, const Act& x) {
   if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
   HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
+  const bool sync = c->sync_fn != nullptr;
   HIPCALL(c, launch_bn_stats_finalize(L.stats_part, M, L.co, conv_nt_stat_rows(S.dt, 0, a), c->stat_scratch,
-                                      c->params + L.g_off, L.st, S.s));
+                                      c->params + L.g_off, L.st, S.s, sync ? c->sync_pack : nullptr));
+  if (sync) {
+    if (int r = sync_exchange(c, c->sync_pack, 2L * L.co, S.s)) return r;
+    HIPCALL(c, launch_bn_sync_unpack(c->sync_pack, L.co, 1.f / c->sync_world, c->params + L.g_off,
+                                     L.st, S.s));
+  }
   return 0;
 }
 
@@ -482,6 +500,13 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
                                     tb ? c->grads + L.g_off : nullptr,
                                     tb ? c->grads + L.b_off : nullptr, S.s));
+  if (c->sync_fn) {
+    // [mean(dyhat) | mean(dyhat * xhat)] (contiguous in the layer's state) averaged over the
+    // replicas: dx is the gradient through the global statistics; dgamma / dbeta stay this
+    // replica's sums (the gradient all-reduce averages them)
+    if (int r = sync_exchange(c, L.st.sdy, 2L * L.co, S.s)) return r;
+    HIPCALL(c, launch_scale2(L.st.sdy, 2L * L.co, 1.f / c->sync_world, 0, 1.f, S.s));
+  }
   const double gb_apply = gb_in + me * esz * (dyhat_out ? 2 : 1);
   if (int r = prof_begin(c, S.s, 5, li, gb_apply, &slot)) return r;
   HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
@@ -743,9 +768,10 @@ int build(seg_ctx* c) {
 
   // ---- activations ----
   const int H = g.height, W = g.width;
+  // the stem input is context-owned in every dtype (the 16-bit tap-8 image, or an fp32 copy):
+  // the stem's weight gradient reads it in seg_backward, after the caller's buffer may be gone
   c->stem8 = seg_half(c->dt);
-  if (c->stem8)
-    if (int r = alloc_act(c, c->img, N, H, W, 8)) return r;
+  if (int r = alloc_act(c, c->img, N, H, W, c->stem8 ? 8 : 3)) return r;
   c->img.N = N; c->img.H = H; c->img.W = W; c->img.C = 3; c->img.ld = c->stem8 ? 8 : 3;
   ConvL& st = c->convs[c->stem];
   if (int r = alloc_conv(c, st, N, H, W)) return r;
@@ -925,10 +951,9 @@ int forward(Step& S, const float* images) {
   seg_ctx* c = S.c;
   if (c->stem8) {
     HIPCALL(c, launch_cast_pad8(S.dt, images, c->img.p, c->img.M(), S.s));
-  } else if (seg_half(c->dt)) {
-    HIPCALL(c, launch_cast_f32_half(c->dt, images, c->img.p, c->img.M() * 3, S.s));
   } else {
-    c->img.p = (void*)images;
+    HIPCALL(c, hipMemcpyAsync(c->img.p, images, (size_t)c->img.M() * 3 * sizeof(float),
+                              hipMemcpyDeviceToDevice, S.s));
   }
   if (int r = conv_forward(S, c->stem, c->img)) return r;
   if (int r = bn_apply(S, c->stem, c->z0, 0)) return r;
@@ -1302,6 +1327,26 @@ int seg_set_loss_scale(seg_ctx* c, float scale) {
   c->loss_scale = scale;
   if (!c->skip_flag && (scale != 1.f || c->dt == SEG_F16))
     if (int r = dalloc(c, &c->skip_flag, 1)) return r;
+  return 0;
+}
+
+int seg_set_bn_sync(seg_ctx* c, seg_allreduce_fn fn, void* user, int world) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (world < 1) return set_err(&c->err, -EINVAL, "world must be >= 1");
+  if (!fn || world == 1) {
+    c->sync_fn = nullptr;
+    c->sync_user = nullptr;
+    c->sync_world = 1;
+    return 0;
+  }
+  if (!c->sync_pack) {
+    int cmax = 1;
+    for (const ConvL& L : c->convs) cmax = std::max(cmax, L.co);
+    if (int r = dalloc(c, &c->sync_pack, 2 * (size_t)cmax)) return r;
+  }
+  c->sync_fn = fn;
+  c->sync_user = user;
+  c->sync_world = world;
   return 0;
 }
 

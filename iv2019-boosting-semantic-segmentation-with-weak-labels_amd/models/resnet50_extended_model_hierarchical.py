@@ -57,7 +57,7 @@ def get_context(config, params, device=None):
     dev = torch.cuda.current_device() if device is None else device
     key = (dev, depth, pyramid, params.height_feature_extractor, params.width_feature_extractor,
            nb_pp, nb_pb, nb_pi, getattr(params, 'compute_dtype', 'bf16'),
-           params.per_pixel_dataset_name)
+           params.per_pixel_dataset_name, bool(getattr(params, 'cross_replica_norm', False)))
     ctx = _CONTEXTS.get(key)
     if ctx is None:
         ctx = SegContext(depth=depth, pyramid=pyramid, height=params.height_feature_extractor,
@@ -70,6 +70,9 @@ def get_context(config, params, device=None):
                          weight_decay=getattr(params, 'regularization_weight', 0.00017),
                          ema=getattr(params, 'ema_decay', 0) > 0, device=dev)
         ctx.load_params(init_params(ctx.param_info, seed=getattr(params, 'init_seed', 0)))
+        if getattr(params, 'cross_replica_norm', False):
+            # hierarchical.py:327-328: BN statistics over all replicas (torch.distributed)
+            ctx.set_bn_sync()
         _CONTEXTS[key] = ctx
     return ctx
 

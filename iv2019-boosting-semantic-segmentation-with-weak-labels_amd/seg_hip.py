@@ -26,7 +26,12 @@ EXPORTED_SYMBOLS = [
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
+    "seg_set_bn_sync",
 ]
+
+# int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, hipStream_t stream)
+SEG_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                    ctypes.c_void_p)
 
 PYRAMID = {"none": 0, "psp": 1, "aspp": 2}
 DTYPE = {"fp32": 0, "bf16": 1, "fp16": 2}
@@ -93,6 +98,7 @@ def _load():
         "seg_stream_wait_bucket": (ip, [vp, ip, vp]),
         "seg_set_loss_scale": (ip, [vp, ctypes.c_float]),
         "seg_found_inf": (ip, [vp, ctypes.POINTER(ctypes.c_void_p)]),
+        "seg_set_bn_sync": (ip, [vp, SEG_ALLREDUCE_FN, vp, ip]),
         "seg_tag_labels": (ip, [vp, ip, ip, ip, vp, vp]),
     }
     for name, (res, args) in sig.items():
@@ -228,6 +234,36 @@ class SegContext:
         p = ctypes.c_void_p()
         check(LIB.seg_found_inf(self.h, ctypes.byref(p)), self.h)
         return None if not p.value else _wrap_i32(p.value, (1,), self.device)
+
+    def set_bn_sync(self, world=None, group=None):
+        """Cross-replica batch norm (the reference's --cross_replica_norm, see seg_set_bn_sync):
+        each BN layer's moments (forward) and gradient means (backward) are summed over
+        `group` by torch.distributed.all_reduce (RCCL or gloo) ordered on the step's stream.
+        world=None takes the group's size; a world of 1 turns synchronisation off."""
+        import torch
+        import torch.distributed as dist
+        if world is None:
+            world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        if world <= 1:
+            check(LIB.seg_set_bn_sync(self.h, SEG_ALLREDUCE_FN(), None, 1), self.h)
+            self._sync_cb = None
+            return
+        dev = self.device
+
+        def _exchange(user, buf, n, stream):   # called from inside seg_forward / seg_backward
+            try:
+                t = _wrap(buf, (int(n),), dev)
+                s = (torch.cuda.ExternalStream(stream, device=dev) if stream
+                     else torch.cuda.default_stream(dev))
+                with torch.cuda.stream(s):
+                    dist.all_reduce(t, group=group)
+                return 0
+            except Exception as e:  # reported through the failing seg_* call
+                self.sync_error = e
+                return 1
+        cb = SEG_ALLREDUCE_FN(_exchange)
+        check(LIB.seg_set_bn_sync(self.h, cb, None, int(world)), self.h)
+        self._sync_cb = cb   # the C side holds the raw pointer: keep the thunk alive
 
     def grad_buckets(self):
         """[(lo, hi)] ranges of self.grads in the order the backward completes them."""

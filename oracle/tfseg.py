@@ -220,14 +220,21 @@ def conv_tf(x, w_ohwi, spec: ConvSpec):
     return F.conv2d(x, w, stride=spec.stride, dilation=spec.rate)
 
 
-def bn_train(y, gamma, beta, eps=BN_EPS):
-    """FusedBatchNorm training: returns (out, batch_mean, batch_var_bessel)."""
+def bn_train(y, gamma, beta, eps=BN_EPS, bessel=True):
+    """FusedBatchNorm training: returns (out, batch_mean, batch_var_bessel).
+
+    bessel=False: the cross-replica path (utils/cross_replica_batch_normalization.py:400-425,
+    run here over the replicas' concatenated batch): normalised by the global mean and the
+    biased global variance, and that biased variance is the moving-average input (:452-466)."""
     n = y.shape[0] * y.shape[2] * y.shape[3]
     mean = y.mean(dim=(0, 2, 3))
-    var = ((y - mean[None, :, None, None]) ** 2).mean(dim=(0, 2, 3))
+    if bessel:
+        var = ((y - mean[None, :, None, None]) ** 2).mean(dim=(0, 2, 3))
+    else:   # the reference's formula (:418): E[x^2] - mean^2
+        var = (y * y).mean(dim=(0, 2, 3)) - mean * mean
     scale = gamma * torch.rsqrt(var + eps)
     out = (y - mean[None, :, None, None]) * scale[None, :, None, None] + beta[None, :, None, None]
-    return out, mean.detach(), (var * (n / max(n - 1, 1))).detach()
+    return out, mean.detach(), (var * (n / max(n - 1, 1)) if bessel else var).detach()
 
 
 def maxpool_same_3x3s2(x):
@@ -336,12 +343,14 @@ class OracleNet:
         self.dtype = dtype
         self.p = {k: torch.tensor(v, dtype=dtype) for k, v in params.items()}
         self.batch_stats: Dict[str, tuple] = {}
+        self.sync_bn = False   # cross-replica BN over a concatenated multi-replica batch
 
     # -- building blocks -------------------------------------------------------------
     def conv_bn(self, x, name: str, relu: Optional[bool] = None, record: Dict = None):
         s = self.spec_by_name[name]
         y = conv_tf(x, self.p[f"{name}/weights"], s)
-        out, m, v = bn_train(y, self.p[f"{name}/BatchNorm/gamma"], self.p[f"{name}/BatchNorm/beta"])
+        out, m, v = bn_train(y, self.p[f"{name}/BatchNorm/gamma"], self.p[f"{name}/BatchNorm/beta"],
+                             bessel=not self.sync_bn)
         self.batch_stats[name] = (m, v)
         if record is not None:
             record[name] = y
@@ -481,15 +490,48 @@ class OracleNet:
 
         Returns (losses, grads-of-seg-loss, new params, new momentum, new ema, batch stats).
         """
+        trainable = self._trainable()
+        low = self.forward(torch.as_tensor(images))
+        L = self.losses(low, px_labels, bbox_soft, tag_soft)
+        return (L, low) + self._grads_and_update(L["segmentation"], trainable, lr, momentum,
+                                                 mom_state, ema_state, ema_decay, step)
+
+    def train_step_replicas(self, batches, lr=0.01, momentum=0.9):
+        """One data-parallel step of R replicas with cross-replica BN (--cross_replica_norm):
+        `batches` = R dicts {images, px, bbox, tag}, each shaped by self.cfg (one replica's
+        sub-batch). BN runs over the R concatenated sub-batches (global mean, biased global
+        variance); each replica's loss is normalised over its own sub-batch; the gradient is
+        that of the replica mean of the losses, i.e. the averaged per-replica gradients of a
+        MirroredStrategy step whose statistics all-reduce is differentiated through.
+        Returns (per-replica losses, grads, new params, new momentum, batch stats)."""
+        self.sync_bn = True
+        try:
+            trainable = self._trainable()
+            imgs = torch.cat([torch.as_tensor(b["images"]) for b in batches], 0)
+            low = self.forward(imgs)
+            nb = self.cfg.nb
+            keys = ("l1_logits", "l2_vehicle_logits", "l2_human_logits")
+            Ls = [self.losses({k: low[k][r * nb:(r + 1) * nb] for k in keys}, b["px"],
+                              b.get("bbox"), b.get("tag"))
+                  for r, b in enumerate(batches)]
+            total = sum(L["segmentation"] for L in Ls) / len(Ls)
+            g, new_p, new_m, _, stats = self._grads_and_update(total, trainable, lr, momentum,
+                                                               None, None, 0.0, 0)
+        finally:
+            self.sync_bn = False
+        return Ls, g, new_p, new_m, stats
+
+    def _trainable(self):
         trainable = {k: v for k, v in self.p.items() if not k.endswith("moving_mean")
                      and not k.endswith("moving_variance")}
         for v in trainable.values():
             v.requires_grad_(True)
-        low = self.forward(torch.as_tensor(images))
-        L = self.losses(low, px_labels, bbox_soft, tag_soft)
+        return trainable
+
+    def _grads_and_update(self, loss, trainable, lr, momentum, mom_state, ema_state, ema_decay,
+                          step):
         names = list(trainable)
-        grads = torch.autograd.grad(L["segmentation"], [trainable[n] for n in names],
-                                    allow_unused=True)
+        grads = torch.autograd.grad(loss, [trainable[n] for n in names], allow_unused=True)
         g = {n: (gr if gr is not None else torch.zeros_like(trainable[n])).detach()
              for n, gr in zip(names, grads)}
         for v in trainable.values():
@@ -512,7 +554,7 @@ class OracleNet:
             mv = self.p[f"{name}/BatchNorm/moving_variance"]
             new_p[f"{name}/BatchNorm/moving_mean"] = mm - (1 - dec) * (mm - m)
             new_p[f"{name}/BatchNorm/moving_variance"] = mv - (1 - dec) * (mv - v)
-        return L, low, g, new_p, new_m, new_e, dict(self.batch_stats)
+        return g, new_p, new_m, new_e, dict(self.batch_stats)
 
 
 # ----------------------------------------------------------------------------------------

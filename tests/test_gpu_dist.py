@@ -70,3 +70,95 @@ def test_bucketed_allreduce_two_ranks_one_gpu():
         assert nb >= 2
         assert err == 0.0, f"rank {rank}: bucketed mean differs by {err}"
     np.testing.assert_array_equal(res[0][2], res[1][2])
+
+
+SYNC_H, SYNC_W = 64, 128
+
+
+def _sync_worker(rank, port, q):
+    """One replica of a cross-replica-BN step (fp32): forward / loss / backward with the BN
+    moments and gradient means exchanged through seg_set_bn_sync (gloo on the device
+    tensors), then the averaged gradient and the update."""
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2",
+                          RANK=str(rank))
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        from estimator.define_estimator_hierarchical import allreduce_grads
+        from input_pipelines.synthetic import batch
+        from oracle.tfseg import SegConfig, init_params
+        from seg_hip import SegContext
+        dev = torch.device("cuda", 0)
+        cfg = SegConfig(height=SYNC_H, width=SYNC_W, nb_pp=1, nb_pb=1, pyramid="psp")
+        params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=3).items()}
+        ctx = SegContext(pyramid="psp", height=SYNC_H, width=SYNC_W, nb_pp=1, nb_pb=1,
+                         dtype="fp32", device=0)
+        ctx.load_params(params)
+        ctx.set_bn_sync()
+        d = batch(40 + rank, 1, 1, 0, SYNC_H, SYNC_W)
+        ctx.forward(torch.as_tensor(d["images"]).to(dev))
+        ctx.loss(torch.as_tensor(d["px"]).to(dev), torch.as_tensor(d["bbox"]).to(dev))
+        ctx.backward()
+        losses, _, _ = ctx.outputs()
+        lv = losses.cpu().numpy()[:4].copy()
+        scale = allreduce_grads(ctx)
+        ctx.apply_update(0.01, 0.9, 0.0, scale)
+        torch.cuda.synchronize()
+        q.put((rank, lv, ctx.named("grads"), ctx.named("params"), None))
+        ctx.set_bn_sync(1)
+        ctx.close()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        q.put((rank, None, None, None, traceback.format_exc() + repr(e)))
+
+
+def test_cross_replica_bn_two_ranks_matches_oracle():
+    """--cross_replica_norm over two replicas (one GPU, gloo) against the oracle's
+    train_step_replicas (BN over both sub-batches, per-replica loss normalisation, gradient of
+    the replica mean): per-replica losses 1e-3, averaged gradients with the conditioning-aware
+    bound of test_gpu_step.test_train_step_fp32, moving statistics 1e-3."""
+    import torch
+    import torch.multiprocessing as mp
+    from input_pipelines.synthetic import batch
+    from oracle.tfseg import OracleNet, SegConfig, init_params
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    port = _free_port()
+    procs = [mctx.Process(target=_sync_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[4] is None, r[4]
+    cfg = SegConfig(height=SYNC_H, width=SYNC_W, nb_pp=1, nb_pb=1, pyramid="psp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=3).items()}
+    batches = [batch(40 + r, 1, 1, 0, SYNC_H, SYNC_W) for r in range(2)]
+    Ls, g, newp, _, _ = OracleNet(cfg, params).train_step_replicas(batches)
+    _, g32, _, _, _ = OracleNet(cfg, params, dtype=torch.float32).train_step_replicas(batches)
+
+    def rel(a, b):
+        a, b = np.asarray(a, np.float64).reshape(-1), np.asarray(b, np.float64).reshape(-1)
+        return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+    for r in range(2):
+        ref = [float(Ls[r][k]) for k in ("segmentation", "l1_segmentation",
+                                         "l2_vehicle_segmentation", "l2_human_segmentation")]
+        np.testing.assert_allclose(res[r][1], ref, rtol=1e-3, atol=1e-6)
+    # both replicas hold the same averaged gradient and the same parameters
+    for k in g:
+        np.testing.assert_array_equal(res[0][2][k], res[1][2][k])
+    for k in res[0][3]:
+        np.testing.assert_array_equal(res[0][3][k], res[1][3][k])
+    errs = {k: rel(res[0][2][k], g[k].numpy()) for k in g}
+    cond = {k: rel(g32[k].numpy(), g[k].numpy()) for k in g}
+    bad = [(errs[k], cond[k], k) for k in g
+           if errs[k] > (max(1e-3, 4 * cond[k]) if cond[k] < 1e-3 else max(5e-2, 2 * cond[k]))]
+    nrm = {k: (float(np.linalg.norm(res[0][2][k])), float(g[k].norm()), float(g32[k].norm()))
+           for _, _, k in bad}
+    assert not bad, (sorted(bad, reverse=True)[:10], nrm)
+    for k, v in newp.items():
+        if "moving" in k:
+            assert rel(res[0][3][k], v.detach().numpy()) < 1e-3, k

@@ -164,3 +164,24 @@ def test_bbox_coordinates_truncate_the_float64_product():
     assert int(np.float32(c) * np.float32(10)) == 7 and int(float(c) * 10) == 6
     rla = generate_bbox_rla([4], np.array([[0.0, c, 0.0, 1.0]], np.float32), (2, 10))
     assert rla[0, 6, 4] == 1.0 and rla[0, 7, 14] == 1.0
+
+
+def test_oracle_cross_replica_bn_duplicate_replicas():
+    """train_step_replicas over two identical replicas is the single-replica step: the same
+    normalisation, the same mean loss and gradient; only the moving-variance input differs
+    (biased global variance instead of the fused op's Bessel-corrected one)."""
+    import torch
+    from input_pipelines.synthetic import batch
+    from oracle.tfseg import OracleNet, SegConfig, init_params
+    cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="psp")
+    params = init_params(cfg, seed=2)
+    b = batch(5, 1, 1, 0, 64, 128)
+    L, _, g, newp, _, _, stats = OracleNet(cfg, params).train_step(b["images"], b["px"], b["bbox"])
+    Ls, g2, newp2, _, stats2 = OracleNet(cfg, params).train_step_replicas([b, b])
+    assert abs(float(Ls[0]["segmentation"]) - float(L["segmentation"])) < 1e-10
+    for k in g:   # float64 summation order differs (2n-row reductions): relative 1e-7
+        assert float((g2[k] - g[k]).norm()) <= 1e-7 * float(g[k].norm()) + 1e-15, k
+    for name, (m, v) in stats.items():
+        torch.testing.assert_close(stats2[name][0], m, rtol=1e-9, atol=1e-10)
+        # biased global variance over 2n samples vs the Bessel-corrected one over n
+        assert torch.all(stats2[name][1] <= v + 1e-12)
