@@ -2,6 +2,13 @@
 #include "bn.h"
 #include <type_traits>
 
+// BN_NT_STORE (A/B): streaming stores for the apply kernels' outputs
+#ifdef BN_NT_STORE
+#define BN_STORE8(T, p, v) store8_nt<T>(p, v)
+#else
+#define BN_STORE8(T, p, v) Vec8<T>::store(p, v)
+#endif
+
 namespace {
 
 // ---- forward statistics: merge per-tile (sum, M2) partials with Chan's formula --------
@@ -367,7 +374,7 @@ __global__ __launch_bounds__(256) void bn_apply8_kernel(BnApplyArgs a) {
         else if constexpr (RES != RES_NONE) x = u[k][e] + x;
         o[e] = RELU ? fmaxf(x, 0.f) : x;
       }
-      Vec8<TO>::store(O + (size_t)(base + k * L.rpp) * a.ldo, o);
+      BN_STORE8(TO, O + (size_t)(base + k * L.rpp) * a.ldo, o);
       if (RELU && a.mask) {   // bits of the value as stored (> 0 after rounding)
         uint32_t bits = 0;
 #pragma unroll
@@ -539,14 +546,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwdArgs a) {
     for (int k = 0; k < BN_U; ++k) {
       if (k >= nrows) continue;
       const size_t m = (size_t)(base + k * L.rpp);
-      if constexpr (HD) Vec8<T>::store(DH + m * a.lddyhat, dz[k]);
+      if constexpr (HD) BN_STORE8(T, DH + m * a.lddyhat, dz[k]);
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xh = (y[k][e] - mu[e]) * inv[e];
         o[e] = sc[e] * (dz[k][e] - sdy[e] - xh * sdyx[e]);
       }
-      Vec8<T>::store(DY + m * a.lddy, o);
+      BN_STORE8(T, DY + m * a.lddy, o);
     }
   };
   long base = (long)blockIdx.x * step + L.rl;

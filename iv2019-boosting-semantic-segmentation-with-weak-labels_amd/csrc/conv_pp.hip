@@ -467,7 +467,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 #ifdef PP_DBG_NOSTORE
       if (v[0] == 1234.5f)
 #endif
-      if (n < a.Co && m < M) Vec8<E>::store(Y + (size_t)m * a.ldy + n, v);
+      if (n < a.Co && m < M) store8_nt(Y + (size_t)m * a.ldy + n, v);
     }
     epi_sync();
 #ifdef PP_DBG_NOSTAGE
@@ -738,7 +738,9 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
   auto mfma_q = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm fragment reads
     __builtin_amdgcn_sched_barrier(0);
+#ifdef PP_WG_DYNPRIO
     __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -746,7 +748,9 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfr[j][s], acc[qm][qn][i][j]);
+#ifdef PP_WG_DYNPRIO
     __builtin_amdgcn_s_setprio(0);
+#endif
   };
   auto wait_next = [&](bool more) {
     if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -762,6 +766,11 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     pp_barrier();
     if (wm == 1) pp_barrier();
+#ifndef PP_WG_DYNPRIO
+    // static priority for the second-dispatched wave row (waves 4-7, the arbitration loser),
+    // no per-segment flips: wgrad 1x1 layers -2..5 % (per-segment flips: PP_WG_DYNPRIO)
+    if (wm == 1) __builtin_amdgcn_s_setprio(1);
+#endif
     for (int kb = 0; kb < nk; ++kb) {
       const bool more = kb + 1 < nk;
       if (more) decode_next();   // K-tile kb + 1

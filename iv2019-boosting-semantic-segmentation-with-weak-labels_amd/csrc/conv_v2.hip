@@ -414,7 +414,7 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += u[e];
           }
-          Vec8<E>::store(Y + (size_t)m * a.ldy + n, v);
+          store8_nt(Y + (size_t)m * a.ldy + n, v);
         }
       }
     }

@@ -98,6 +98,31 @@ template <> struct Vec8<f16_t> {
   }
 };
 
+// 8 values -> one 16-byte non-temporal store (conv outputs: written once, read by the next
+// kernel from HBM anyway; the streaming hint lets the epilogue's stores drain sooner)
+template <typename E>
+__device__ __forceinline__ void store8_nt(E* p, const float* v) {
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  if constexpr (sizeof(E) == 4) {
+    typedef float f32x4v_t __attribute__((ext_vector_type(4)));
+    const f32x4v_t a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+    __builtin_nontemporal_store(a, (f32x4v_t*)p);
+    __builtin_nontemporal_store(b, (f32x4v_t*)(p + 4));
+  } else {
+    u32x4_t w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const E lo = TypeOps<E>::from_f(v[2 * i]), hi = TypeOps<E>::from_f(v[2 * i + 1]);
+      uint16_t bl, bh;
+      __builtin_memcpy(&bl, &lo, 2);
+      __builtin_memcpy(&bh, &hi, 2);
+      w[i] = (uint32_t)bl | ((uint32_t)bh << 16);
+    }
+    __builtin_nontemporal_store(w, (u32x4_t*)p);
+  }
+}
+
+
 // 16-bit element traits of the MFMA kernels: fragment vector type, the 16x16x32 MFMA, and
 // the unpack of a raw 16-byte chunk
 template <typename E> struct Half;
