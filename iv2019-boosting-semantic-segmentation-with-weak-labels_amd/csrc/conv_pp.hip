@@ -26,6 +26,15 @@
 #include "conv.h"
 #include <cstdlib>
 
+#ifdef PP_DBG_TIMING
+// A/B only: per-block, per-tile timestamps (s_memtime) of the NT persistent loop
+__device__ unsigned long long g_pp_dbg[256 * 16 * 4];
+#define PP_TS(it, k) \
+  if (threadIdx.x == 0 && blockIdx.x < 256 && (it) < 16) g_pp_dbg[(blockIdx.x * 16 + (it)) * 4 + (k)] = __builtin_amdgcn_s_memtime()
+#else
+#define PP_TS(it, k)
+#endif
+
 namespace {
 
 constexpr int PP_THREADS = 512;
@@ -33,7 +42,7 @@ constexpr int PBK = 64;                    // 16-bit K-elements per K-tile (128-
 constexpr int HALF = 128 * 128;            // one half-tile: 128 rows x 128 B
 constexpr int BUF = 4 * HALF;              // A0 A1 B0 B1
 constexpr int PP_LDS = 2 * BUF;            // 128 KB
-constexpr int EPI_COLS = 64, EPI_LD = EPI_COLS + 4;
+constexpr int EPI_COLS = 64, EPI_LD = EPI_COLS + 4;   // fp32 staging (residual epilogue)
 
 __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
 
@@ -44,6 +53,20 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
+}
+
+// one butterfly step of per-channel (sum, M2) pairs between DPP partner lanes, equal counts n
+template <int CTRL>
+__device__ __forceinline__ void chan_step(float (&sm)[4], float (&m2)[4], float n) {
+  const float inv = 1.f / n, hn = 0.5f * n;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float s2 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sm[r]), CTRL, 0xf, 0xf, false));
+    const float q2 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, m2[r]), CTRL, 0xf, 0xf, false));
+    const float d = (s2 - sm[r]) * inv;
+    m2[r] = m2[r] + q2 + d * d * hn;
+    sm[r] += s2;
+  }
 }
 
 // PERSIST: loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
@@ -102,7 +125,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
-      const int row = (j >> 1) * 128 + rr;
+      // LDS half h = j >> 1, position rr -> tile row. Persistent: wave row rr / 64 owns the
+      // contiguous tile rows [128 * (rr / 64), +128) (quadrant qm = h: rows qm * 64 + 0..63)
+      const int row = PERSIST ? (rr >> 6) * 128 + (j >> 1) * 64 + (rr & 63) : (j >> 1) * 128 + rr;
       a_lc[j] = swz(rr, pc);
       const long m = m0_ + row;
       const bool ok = m < M;
@@ -114,6 +139,10 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       a_h0[j] = ok ? ho * a.sf - a.pad_h : -(1 << 28);
       a_w0[j] = wo * a.sf - a.pad_w;
       a_voff[j] = (((int)(a_nb[j] + a_h0[j]) * a.W + a_w0[j]) * a.ldx + a_lc[j] * 8) * 2;
+#ifdef PP_DBG_AROWS
+      // A/B only: every tile reads the A rows of tile 0 (L2-resident source, same LDS image shape)
+      a_voff[j] = ((int)((row % PP_DBG_AROWS) * a.ldx) + a_lc[j] * 8) * 2;
+#endif
       int bits = 0;
       for (int q = 0; q < a.KH; ++q) bits |= ((unsigned)(a_h0[j] + q * a.dil) < (unsigned)a.H) << q;
       for (int q = 0; q < a.KW; ++q) bits |= ((unsigned)(a_w0[j] + q * a.dil) < (unsigned)a.W) << (4 + q);
@@ -203,7 +232,10 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfr[j][s], acc[qm][qn][i][j]);
+          // persistent: transposed accumulators (lane = 4 channels of one pixel) for the
+          // register-side statistics and 8-byte staging writes; else the v2 layout
+          acc[qm][qn][i][j] = PERSIST ? Half<E>::mma(bfr[j][s], af[i][s], acc[qm][qn][i][j])
+                                      : Half<E>::mma(af[i][s], bfr[j][s], acc[qm][qn][i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -218,7 +250,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     issue_half(0, t0, 1);
   };
   prologue();
+  int dbg_it = 0; (void)dbg_it;
   for (;;) {   // ---- persistent tile loop ----
+  PP_TS(dbg_it, 0);
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
@@ -276,8 +310,8 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     pp_barrier();
   }
   if (wm == 0) pp_barrier();   // realign the two wave rows: every LDS read of the tile is done
-  // next tile: its K-tile 0 goes into buffer 0 now, in flight during this tile's epilogue,
-  // which stages through the buffer-1 region
+  PP_TS(dbg_it, 1);
+  // next tile: its K-tile 0 goes into buffer 0 now, in flight during this tile's epilogue
   const int tile_n = tile + (int)gridDim.x;
   const bool has_next = PERSIST && tile_n < nwg;
   int mt_n = 0, nt_n = 0;
@@ -286,194 +320,350 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     setup_lanes((long)mt_n * BM, nt_n * BN);
     prologue();
   }
-  // LDS hand-off inside the epilogue: raw barrier after the LDS writes retire (a
-  // __syncthreads would also wait for the next tile's DMA)
-  auto epi_sync = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    pp_barrier();
-  };
-  char* const epi = smem + BUF;
+  if constexpr (PERSIST) {
+      // ---- persistent epilogue: transposed accumulators (mfma(B, A)): lane (lq, lr) of
+      // fragment acc[qm][qn][i][j] holds output pixel m = m0 + wm*128 + qm*64 + i*16 + lr and
+      // the four channels n = n0 + qn*128 + wn*32 + j*16 + lq*4 + 0..3
+    const long mw = m0 + wm * 128;                      // this wave row's 128 contiguous rows
+    const long mrows = M - mw;
+    const int nvalid = (int)(mrows < 0 ? 0 : (mrows < 128 ? mrows : 128));
+    const int nbase = n0 + wn * 32 + lq * 4;
+    if (a.stats && nvalid > 0) {
+      // per channel (sum, M2) over the wave row's rows: 8 values in the lane, then a butterfly
+      // over the 16 lanes (lr) holding the same channels; one partial per 128 rows
+      // (conv_nt_stat_rows); the ragged last tile merges with per-lane counts
+      const bool full = nvalid == 128;
+  #pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+  #pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float sm[4], m2[4];
+          if (full) {
+            // 8 rows in the lane: exact two-pass moments, then a DPP butterfly over the 16
+            // lanes of the row group (pairs via quad_perm xor 1, xor 2, row_half_mirror,
+            // row_mirror), equal counts 8 -> 64: M2 += d^2 * n / 2 with d = (s_b - s_a) / n
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float s_ = 0.f;
+  #pragma unroll
+              for (int qm = 0; qm < 2; ++qm)
+  #pragma unroll
+                for (int i = 0; i < 4; ++i) s_ += acc[qm][qn][i][j][r];
+              const float mu = s_ * 0.125f;
+              float q_ = 0.f;
+  #pragma unroll
+              for (int qm = 0; qm < 2; ++qm)
+  #pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const float d = acc[qm][qn][i][j][r] - mu;
+                  q_ = __builtin_fmaf(d, d, q_);
+                }
+              sm[r] = s_;
+              m2[r] = q_;
+            }
+            chan_step<0xB1>(sm, m2, 8.f);
+            chan_step<0x4E>(sm, m2, 16.f);
+            chan_step<0x141>(sm, m2, 32.f);
+            chan_step<0x140>(sm, m2, 64.f);
+          } else {
+            // ragged last tile: per-lane counts, general merges
+            int c = 0;
+  #pragma unroll
+            for (int qm = 0; qm < 2; ++qm)
+  #pragma unroll
+              for (int i = 0; i < 4; ++i) c += (qm * 64 + i * 16 + lr) < nvalid;
+            const float cnt = (float)c;
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float s_ = 0.f;
+  #pragma unroll
+              for (int qm = 0; qm < 2; ++qm)
+  #pragma unroll
+                for (int i = 0; i < 4; ++i)
+                  s_ += (qm * 64 + i * 16 + lr) < nvalid ? acc[qm][qn][i][j][r] : 0.f;
+              const float mu = cnt > 0.f ? s_ / cnt : 0.f;
+              float q_ = 0.f;
+  #pragma unroll
+              for (int qm = 0; qm < 2; ++qm)
+  #pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const float d = acc[qm][qn][i][j][r] - mu;
+                  q_ += (qm * 64 + i * 16 + lr) < nvalid ? d * d : 0.f;
+                }
+              sm[r] = s_;
+              m2[r] = q_;
+            }
+            float nn = cnt;
+  #pragma unroll
+            for (int o = 1; o <= 8; o <<= 1) {
+              const float n2 = __shfl_xor(nn, o, 64);
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float s2 = __shfl_xor(sm[r], o, 64), q2 = __shfl_xor(m2[r], o, 64);
+                const float tot = nn + n2;
+                const float d = (n2 > 0.f && nn > 0.f) ? s2 / n2 - sm[r] / nn : 0.f;
+                m2[r] = m2[r] + q2 + (tot > 0.f ? d * d * (nn * n2 / tot) : 0.f);
+                sm[r] += s2;
+              }
+              nn = nn + n2;
+            }
+          }
+          const int n = nbase + qn * 128 + j * 16;
+          if (lr == 0 && n < a.Co) {
+            float* dst = a.stats + 2 * ((size_t)(mt * 2 + wm) * a.Co + n);
+            *(float4*)dst = make_float4(sm[0], m2[0], sm[1], m2[1]);
+            *(float4*)(dst + 4) = make_float4(sm[2], m2[2], sm[3], m2[3]);
+          }
+        }
+    }
+    PP_TS(dbg_it, 2);
+    // output: packed to 16-bit in registers, staged one 128-column half at a time through the
+    // buffer-1 region (row-major, 16-B chunks XOR-swizzled by row: conflict-free 8-B writes
+    // and 16-B reads), then 16 B per lane, 256 contiguous bytes per row, streaming stores
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    auto pack4 = [](const f32x4_t& v) {
+      u32x2_t w;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const E lo = TypeOps<E>::from_f(v[2 * h]), hi = TypeOps<E>::from_f(v[2 * h + 1]);
+        uint16_t bl, bh;
+        __builtin_memcpy(&bl, &lo, 2);
+        __builtin_memcpy(&bh, &hi, 2);
+        w[h] = (uint32_t)bl | ((uint32_t)bh << 16);
+      }
+      return w;
+    };
+    char* const stg = smem + BUF;
+    E* Y = (E*)a.y;
+    const int s_row = tid >> 4, s_ch = tid & 15;
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn) {
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int row = wm * 128 + qm * 64 + i * 16 + lr;
+            const int ch = wn * 4 + j * 2 + (lq >> 1);
+            *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) =
+                pack4(acc[qm][qn][i][j]);
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      u32x4_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int row = k * 32 + s_row;
+        v[k] = *(const u32x4_t*)(stg + row * 256 + ((s_ch ^ (row & 15)) << 4));
+      }
+      const int n = n0 + qn * 128 + s_ch * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const long m = m0 + k * 32 + s_row;
+#ifdef PP_DBG_NOSTORE
+        if (v[k][0] == 0x12345678u)
+#endif
+        if (m < M && n < a.Co) __builtin_nontemporal_store(v[k], (u32x4_t*)(Y + (size_t)m * a.ldy + n));
+      }
+      if (qn == 0) {   // the second half overwrites the staging area
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_barrier();
+      }
+    }
+  } else {
+    // LDS hand-off inside the epilogue: raw barrier after the LDS writes retire (a
+    // __syncthreads would also wait for the next tile's DMA)
+    auto epi_sync = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+    };
+    char* const epi = smem + BUF;
 
-  // ---- epilogue (as conv_nt_v2_kernel): flat fragment view fi' = qm*4 + fi, fj' = qn*2 + fj
-  constexpr int FM = 8, FN = 4, WMW = 2, WM = 128;
-  auto A_ = [&](int fi, int fj) -> f32x4_t& { return acc[fi >> 2][fj >> 1][fi & 3][fj & 1]; };
-  auto row_of = [&](int fi, int k) { return (fi >> 2) * 128 + wm * 64 + (fi & 3) * 16 + lq * 4 + k; };
-  auto col_of = [&](int fj) { return (fj >> 1) * 128 + wn * 32 + (fj & 1) * 16 + lr; };
-  const bool col_writer = lq == 0;
-  const int rows_valid = (int)((M - m0) < BM ? (M - m0) : BM);
-  float* red = (float*)epi;
-  if (a.stats && rows_valid == BM) {
-    float2* red2 = (float2*)epi;
-    constexpr float NL = (float)(4 * FM);
-    float sj[FN], mj[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float sm = 0.f, sq = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float x = A_(i, j)[k];
-          sm += x;
-          sq = __builtin_fmaf(x, x, sq);
-        }
-      sj[j] = sm;
-      mj[j] = fmaxf(sq - sm * sm * (1.f / NL), 0.f);
-    }
-    float n = NL;
-#pragma unroll
-    for (int o = 16; o <= 32; o <<= 1) {
-#pragma unroll
+    // ---- epilogue (as conv_nt_v2_kernel): flat fragment view fi' = qm*4 + fi, fj' = qn*2 + fj
+    constexpr int FM = 8, FN = 4, WMW = 2, WM = 128;
+    auto A_ = [&](int fi, int fj) -> f32x4_t& { return acc[fi >> 2][fj >> 1][fi & 3][fj & 1]; };
+    auto row_of = [&](int fi, int k) { return (fi >> 2) * 128 + wm * 64 + (fi & 3) * 16 + lq * 4 + k; };
+    auto col_of = [&](int fj) { return (fj >> 1) * 128 + wn * 32 + (fj & 1) * 16 + lr; };
+    const bool col_writer = lq == 0;
+    const int rows_valid = (int)((M - m0) < BM ? (M - m0) : BM);
+    float* red = (float*)epi;
+    if (a.stats && rows_valid == BM) {
+      float2* red2 = (float2*)epi;
+      constexpr float NL = (float)(4 * FM);
+      float sj[FN], mj[FN];
+  #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
-        const float d = (s2 - sj[j]) / n;
-        mj[j] = mj[j] + m2 + d * d * (0.5f * n);
-        sj[j] += s2;
+        float sm = 0.f, sq = 0.f;
+  #pragma unroll
+        for (int i = 0; i < FM; ++i)
+  #pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float x = A_(i, j)[k];
+            sm += x;
+            sq = __builtin_fmaf(x, x, sq);
+          }
+        sj[j] = sm;
+        mj[j] = fmaxf(sq - sm * sm * (1.f / NL), 0.f);
       }
-      n *= 2.f;
-    }
-    if (col_writer)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
-    epi_sync();
-    if (wm == 0 && col_writer) {
-#pragma unroll
+      float n = NL;
+  #pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
+          const float d = (s2 - sj[j]) / n;
+          mj[j] = mj[j] + m2 + d * d * (0.5f * n);
+          sj[j] += s2;
+        }
+        n *= 2.f;
+      }
+      if (col_writer)
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
+      epi_sync();
+      if (wm == 0 && col_writer) {
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c = col_of(j);
+          float2 t = red2[c];
+          float ntot = (float)WM;
+  #pragma unroll
+          for (int w = 1; w < WMW; ++w) {
+            const float2 u = red2[w * BN + c];
+            const float d = u.x / (float)WM - t.x / ntot;
+            t.y = t.y + u.y + d * d * (ntot * (float)WM / (ntot + (float)WM));
+            t.x += u.x;
+            ntot += (float)WM;
+          }
+          if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = t;
+        }
+      }
+      epi_sync();
+    } else if (a.stats) {
+      float cs[FN];
+  #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int c = col_of(j);
-        float2 t = red2[c];
-        float ntot = (float)WM;
-#pragma unroll
-        for (int w = 1; w < WMW; ++w) {
-          const float2 u = red2[w * BN + c];
-          const float d = u.x / (float)WM - t.x / ntot;
-          t.y = t.y + u.y + d * d * (ntot * (float)WM / (ntot + (float)WM));
-          t.x += u.x;
-          ntot += (float)WM;
-        }
-        if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = t;
+        float v = 0.f;
+  #pragma unroll
+        for (int i = 0; i < FM; ++i)
+  #pragma unroll
+          for (int k = 0; k < 4; ++k) v += row_of(i, k) < rows_valid ? A_(i, j)[k] : 0.f;
+  #pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
+        cs[j] = v;
       }
-    }
-    epi_sync();
-  } else if (a.stats) {
-    float cs[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float v = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v += row_of(i, k) < rows_valid ? A_(i, j)[k] : 0.f;
-#pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
-      cs[j] = v;
-    }
-    if (col_writer)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
-    epi_sync();
-    float mean[FN], tot[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int c = col_of(j);
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
-      tot[j] = t;
-      mean[j] = t / (float)rows_valid;
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float v = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float d = A_(i, j)[k] - mean[j];
-          v += row_of(i, k) < rows_valid ? d * d : 0.f;
-        }
-#pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
-      cs[j] = v;
-    }
-    epi_sync();
-    if (col_writer)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
-    epi_sync();
-    if (wm == 0 && col_writer) {
-#pragma unroll
+      if (col_writer)
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
+      epi_sync();
+      float mean[FN], tot[FN];
+  #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int c = col_of(j);
         float t = 0.f;
-#pragma unroll
+  #pragma unroll
         for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
-        if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = make_float2(tot[j], t);
+        tot[j] = t;
+        mean[j] = t / (float)rows_valid;
       }
-    }
-    epi_sync();
-  }
-  float* stage = (float*)epi;
-  E* Y = (E*)a.y;
-  const E* R1 = (const E*)a.r;
-  const E* R2 = (const E*)a.r2;
-  const int s_rl = tid >> 3, s_cc = tid & 7;
-  // residual operands (dgrad): one pass's rows are loaded into registers before its
-  // accumulators are staged, all loads unconditional (rows past M clamped), so they are in
-  // flight together with the LDS staging and cost one wait per pass (a per-row conditional
-  // load made hipcc wait vmcnt(0) after every load)
-  // (persistent launches carry no residuals: pp_launch_st routes those to PERSIST = 0)
-  const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
-  auto bf8_add = [](float* v, const uint4 u) {
-    float w[8];
-    Half<E>::unpack(u, w);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] += w[i];
-  };
-#pragma unroll
-  for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
-    const int cbase = pass * EPI_COLS;
-    const int n = n0 + cbase + s_cc * 8;
-    const int nc = n < a.Co ? n : 0;
-    uint4 r1v[BM / 64], r2v[BM / 64];
-    if (nres) {
-#pragma unroll
-      for (int rr = 0; rr < BM / 64; ++rr) {
-        const long m = m0 + s_rl + 64 * rr;
-        const long mc = m < M ? m : M - 1;
-        r1v[rr] = *(const uint4*)(R1 + (size_t)mc * a.ldr + nc);
-        if (nres == 2) r2v[rr] = *(const uint4*)(R2 + (size_t)mc * a.ldr2 + nc);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = col_of(j);
-      if (col >= cbase && col < cbase + EPI_COLS) {
-#pragma unroll
+  #pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float v = 0.f;
+  #pragma unroll
         for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = A_(i, j)[k];
+  #pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float d = A_(i, j)[k] - mean[j];
+            v += row_of(i, k) < rows_valid ? d * d : 0.f;
+          }
+  #pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
+        cs[j] = v;
       }
+      epi_sync();
+      if (col_writer)
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
+      epi_sync();
+      if (wm == 0 && col_writer) {
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c = col_of(j);
+          float t = 0.f;
+  #pragma unroll
+          for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
+          if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = make_float2(tot[j], t);
+        }
+      }
+      epi_sync();
     }
-    epi_sync();
-#pragma unroll
-    for (int rr = 0; rr < BM / 64; ++rr) {
-      const int row = s_rl + 64 * rr;
-      const long m = m0 + row;
-      const float* sp = stage + row * EPI_LD + s_cc * 8;
-      const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
-      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if (nres) bf8_add(v, r1v[rr]);
-      if (nres == 2) bf8_add(v, r2v[rr]);
-#ifdef PP_DBG_NOSTORE
-      if (v[0] == 1234.5f)
-#endif
-      if (n < a.Co && m < M) store8_nt(Y + (size_t)m * a.ldy + n, v);
+    float* stage = (float*)epi;
+    E* Y = (E*)a.y;
+    const E* R1 = (const E*)a.r;
+    const E* R2 = (const E*)a.r2;
+    const int s_rl = tid >> 3, s_cc = tid & 7;
+    // residual operands (dgrad): one pass's rows are loaded into registers before its
+    // accumulators are staged, all loads unconditional (rows past M clamped), so they are in
+    // flight together with the LDS staging and cost one wait per pass (a per-row conditional
+    // load made hipcc wait vmcnt(0) after every load)
+    // (persistent launches carry no residuals: pp_launch_st routes those to PERSIST = 0)
+    const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
+    auto bf8_add = [](float* v, const uint4 u) {
+      float w[8];
+      Half<E>::unpack(u, w);
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += w[i];
+    };
+  #pragma unroll
+    for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
+      const int cbase = pass * EPI_COLS;
+      const int n = n0 + cbase + s_cc * 8;
+      const int nc = n < a.Co ? n : 0;
+      uint4 r1v[BM / 64], r2v[BM / 64];
+      if (nres) {
+  #pragma unroll
+        for (int rr = 0; rr < BM / 64; ++rr) {
+          const long m = m0 + s_rl + 64 * rr;
+          const long mc = m < M ? m : M - 1;
+          r1v[rr] = *(const uint4*)(R1 + (size_t)mc * a.ldr + nc);
+          if (nres == 2) r2v[rr] = *(const uint4*)(R2 + (size_t)mc * a.ldr2 + nc);
+        }
+      }
+  #pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = col_of(j);
+        if (col >= cbase && col < cbase + EPI_COLS) {
+  #pragma unroll
+          for (int i = 0; i < FM; ++i)
+  #pragma unroll
+            for (int k = 0; k < 4; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = A_(i, j)[k];
+        }
+      }
+      epi_sync();
+  #pragma unroll
+      for (int rr = 0; rr < BM / 64; ++rr) {
+        const int row = s_rl + 64 * rr;
+        const long m = m0 + row;
+        const float* sp = stage + row * EPI_LD + s_cc * 8;
+        const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
+        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        if (nres) bf8_add(v, r1v[rr]);
+        if (nres == 2) bf8_add(v, r2v[rr]);
+  #ifdef PP_DBG_NOSTORE
+        if (v[0] == 1234.5f)
+  #endif
+        if (n < a.Co && m < M) store8_nt(Y + (size_t)m * a.ldy + n, v);
+      }
+      epi_sync();
+  #ifdef PP_DBG_NOSTAGE
+      break;
+  #endif
     }
-    epi_sync();
-#ifdef PP_DBG_NOSTAGE
-    break;
-#endif
   }
+  PP_TS(dbg_it, 3);
+  ++dbg_it;
   if (!has_next) break;
   tile = tile_n;
   mt = mt_n;
@@ -504,7 +694,8 @@ int pp_grid(int nwg) {
 
 template <typename E, int ST, int PERSIST>
 hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
-  constexpr int LDS = BUF + 256 * EPI_LD * 4;   // ring buffer 0 + (buffer 1 | epilogue staging)
+  // two K-tile buffers; the fp32 staging of the residual (non-persistent) epilogue needs more
+  constexpr int LDS = PERSIST ? PP_LDS : BUF + 256 * EPI_LD * 4;
   static_assert(LDS >= PP_LDS && LDS <= 160 * 1024, "LDS budget");
   auto kern = conv_nt_pp_kernel<E, ST, PERSIST>;
   static bool attr = false;
@@ -530,7 +721,9 @@ hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
 // ping-pong config: the v2 fast-path preconditions (conv_nt_v2_ok, no tap8), Co > 128 and an
 // operands of < 2^31 bytes (32-bit buffer offsets), kernels up to 4 x 4 (tap validity bits)
 bool conv_nt_pp_ok(const ConvArgs& a) {
-  return !a.tap8 && a.Co > 128 && a.KH <= 4 && a.KW <= 4 && conv_nt_v2_ok(a) &&
+  // 16-byte epilogue stores: channel counts and row strides multiples of 8
+  return !a.tap8 && a.Co > 128 && a.Co % 8 == 0 && a.ldy % 8 == 0 &&
+         a.KH <= 4 && a.KW <= 4 && conv_nt_v2_ok(a) &&
          (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31) && (long)a.Co * a.ldw * 2 < (1L << 31);
 }
 
@@ -855,3 +1048,9 @@ hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s) {
   if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<bf16_t, 1>);
   return launch(conv_wgrad_pp_kernel<bf16_t, 0>);
 }
+
+#ifdef PP_DBG_TIMING
+extern "C" int seg_dbg_pp_timing(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pp_dbg), sizeof(g_pp_dbg)) == hipSuccess ? 0 : -1;
+}
+#endif

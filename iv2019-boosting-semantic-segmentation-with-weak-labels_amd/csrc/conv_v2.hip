@@ -466,7 +466,8 @@ bool conv_nt_v2_ok(const ConvArgs& a) {
 // (Measured and rejected: 128 x 128 tiles with a 64 KB ring, two workgroups per CU, for short
 // reductions K <= 512 -- 10-20 % slower than 256-row tiles on the C2 1x1 layers.)
 int conv_nt_v2_rows(const ConvArgs& a) {
-  (void)a;
+  // the ping-pong kernel writes one partial per wave row (128 rows), the v2 kernels per tile
+  if (a.Co > 128 && !a.r && !a.r2 && conv_nt_pp_enabled() && conv_nt_pp_ok(a)) return 128;
   return 256;
 }
 
