@@ -129,23 +129,30 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       // contiguous tile rows [128 * (rr / 64), +128) (quadrant qm = h: rows qm * 64 + 0..63)
       const int row = PERSIST ? (rr >> 6) * 128 + (j >> 1) * 64 + (rr & 63) : (j >> 1) * 128 + rr;
       a_lc[j] = swz(rr, pc);
-      const long m = m0_ + row;
-      const bool ok = m < M;
-      const long mm = ok ? m : 0;
-      const int wo = (int)(mm % a.Wo);
-      const long t = mm / a.Wo;
-      const int ho = (int)(t % a.Ho);
-      a_nb[j] = (t / a.Ho) * a.H;
+      // 32-bit index math (M, N*H*W < 2^31: host check): 64-bit div/rem per row was ~1/3 of
+      // the per-tile setup on short-K layers
+      const int m = (int)m0_ + row;
+      const bool ok = m < (int)M;
+      const unsigned mm = ok ? (unsigned)m : 0u;
+      const unsigned t = mm / (unsigned)a.Wo;
+      const int wo = (int)(mm - t * (unsigned)a.Wo);
+      const unsigned nimg = t / (unsigned)a.Ho;
+      const int ho = (int)(t - nimg * (unsigned)a.Ho);
+      a_nb[j] = (long)(nimg * (unsigned)a.H);
       a_h0[j] = ok ? ho * a.sf - a.pad_h : -(1 << 28);
       a_w0[j] = wo * a.sf - a.pad_w;
-      a_voff[j] = (((int)(a_nb[j] + a_h0[j]) * a.W + a_w0[j]) * a.ldx + a_lc[j] * 8) * 2;
+      a_voff[j] = (((int)a_nb[j] + a_h0[j]) * a.W + a_w0[j]) * a.ldx * 2 + a_lc[j] * 16;
 #ifdef PP_DBG_AROWS
       // A/B only: every tile reads the A rows of tile 0 (L2-resident source, same LDS image shape)
       a_voff[j] = ((int)((row % PP_DBG_AROWS) * a.ldx) + a_lc[j] * 8) * 2;
 #endif
       int bits = 0;
-      for (int q = 0; q < a.KH; ++q) bits |= ((unsigned)(a_h0[j] + q * a.dil) < (unsigned)a.H) << q;
-      for (int q = 0; q < a.KW; ++q) bits |= ((unsigned)(a_w0[j] + q * a.dil) < (unsigned)a.W) << (4 + q);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < a.KH) bits |= ((unsigned)(a_h0[j] + q * a.dil) < (unsigned)a.H) << q;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < a.KW) bits |= ((unsigned)(a_w0[j] + q * a.dil) < (unsigned)a.W) << (4 + q);
       a_bits[j] = bits;
     }
     // B rows: half g, instruction i -> output channel n0 + g*128 + (i*8+wave)*8 + lane/8
@@ -328,13 +335,13 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     const long mrows = M - mw;
     const int nvalid = (int)(mrows < 0 ? 0 : (mrows < 128 ? mrows : 128));
     const int nbase = n0 + wn * 32 + lq * 4;
-    if (a.stats && nvalid > 0) {
-      // per channel (sum, M2) over the wave row's rows: 8 values in the lane, then a butterfly
-      // over the 16 lanes (lr) holding the same channels; one partial per 128 rows
-      // (conv_nt_stat_rows); the ragged last tile merges with per-lane counts
-      const bool full = nvalid == 128;
-  #pragma unroll
-      for (int qn = 0; qn < 2; ++qn)
+    // per channel (sum, M2) over the wave row's rows: 8 values in the lane, then a butterfly
+    // over the 16 lanes (lr) holding the same channels; one partial per 128 rows
+    // (conv_nt_stat_rows); the ragged last tile merges with per-lane counts. Run per column
+    // half between that half's staging writes and the barrier, so the VALU work overlaps the
+    // LDS traffic and the other waves' arrival
+    const bool full = nvalid == 128;
+    auto stats_half = [&](const int qn) {
   #pragma unroll
         for (int j = 0; j < 2; ++j) {
           float sm[4], m2[4];
@@ -415,7 +422,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             *(float4*)(dst + 4) = make_float4(sm[2], m2[2], sm[3], m2[3]);
           }
         }
-    }
+    };
     PP_TS(dbg_it, 2);
     // output: packed to 16-bit in registers, staged one 128-column half at a time through the
     // buffer-1 region (row-major, 16-B chunks XOR-swizzled by row: conflict-free 8-B writes
@@ -450,6 +457,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) =
                 pack4(acc[qm][qn][i][j]);
           }
+      if (a.stats && nvalid > 0) stats_half(qn);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       pp_barrier();
       u32x4_t v[8];
@@ -724,7 +732,8 @@ bool conv_nt_pp_ok(const ConvArgs& a) {
   // 16-byte epilogue stores: channel counts and row strides multiples of 8
   return !a.tap8 && a.Co > 128 && a.Co % 8 == 0 && a.ldy % 8 == 0 &&
          a.KH <= 4 && a.KW <= 4 && conv_nt_v2_ok(a) &&
-         (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31) && (long)a.Co * a.ldw * 2 < (1L << 31);
+         (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31) && (long)a.Co * a.ldw * 2 < (1L << 31) &&
+         (long)a.N * a.Ho * a.Wo < (1L << 31);   // 32-bit pixel indices
 }
 
 template <typename E>
