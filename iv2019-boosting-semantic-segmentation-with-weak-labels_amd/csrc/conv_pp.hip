@@ -56,6 +56,7 @@ __device__ __forceinline__ void pp_barrier() {
 }
 
 // one butterfly step of per-channel (sum, M2) pairs between DPP partner lanes, equal counts n
+// (scalar: a DPP move feeding packed fp32 math miscompiled for lanes 1-3 of the vector)
 template <int CTRL>
 __device__ __forceinline__ void chan_step(float (&sm)[4], float (&m2)[4], float n) {
   const float inv = 1.f / n, hn = 0.5f * n;
@@ -349,24 +350,20 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             // 8 rows in the lane: exact two-pass moments, then a DPP butterfly over the 16
             // lanes of the row group (pairs via quad_perm xor 1, xor 2, row_half_mirror,
             // row_mirror), equal counts 8 -> 64: M2 += d^2 * n / 2 with d = (s_b - s_a) / n
-  #pragma unroll
+            f32x4_t s4 = acc[0][qn][0][j];
+#pragma unroll
+            for (int f = 1; f < 8; ++f) s4 += acc[f >> 2][qn][f & 3][j];
+            const f32x4_t mu = s4 * 0.125f;
+            f32x4_t q4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int f = 0; f < 8; ++f) {
+              const f32x4_t d = acc[f >> 2][qn][f & 3][j] - mu;
+              q4 += d * d;
+            }
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float s_ = 0.f;
-  #pragma unroll
-              for (int qm = 0; qm < 2; ++qm)
-  #pragma unroll
-                for (int i = 0; i < 4; ++i) s_ += acc[qm][qn][i][j][r];
-              const float mu = s_ * 0.125f;
-              float q_ = 0.f;
-  #pragma unroll
-              for (int qm = 0; qm < 2; ++qm)
-  #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                  const float d = acc[qm][qn][i][j][r] - mu;
-                  q_ = __builtin_fmaf(d, d, q_);
-                }
-              sm[r] = s_;
-              m2[r] = q_;
+              sm[r] = s4[r];
+              m2[r] = q4[r];
             }
             chan_step<0xB1>(sm, m2, 8.f);
             chan_step<0x4E>(sm, m2, 16.f);
