@@ -1,5 +1,6 @@
 // Batch-norm kernels (see bn.h). All reductions use a fixed order: bitwise reproducible.
 #include "bn.h"
+#include <cstdlib>
 #include <type_traits>
 
 // BN_NT_STORE (A/B): streaming stores for the apply kernels' outputs
@@ -71,6 +72,93 @@ __global__ void bn_stats_stage2(const float* __restrict__ g, int G, int C, const
   if (pack) {   // this replica's moments for the cross-replica exchange
     pack[c] = mean;
     pack[C + c] = var + mean * mean;
+  }
+}
+
+// one-launch finalize of the forward statistics (replaces stage1 + stage2): per-tile (sum, M2)
+// partials of tile_rows rows (the last one ragged) merged as shifted sums around tile 0's mean
+// p: A = sum_t n_t (mean_t - p), B = sum_t (M2_t + n_t (mean_t - p)^2), so mean = p + A / N and
+// var = B / N - (A / N)^2, with no division per merge; 8 channels x 64 tile lanes per block,
+// fixed summation order (bitwise reproducible)
+constexpr int SF_CH = 8, SF_LANES = 64;
+constexpr int BF_CH = 8, BF_LANES = 64;   // backward finalize: more blocks, shorter loops
+__global__ __launch_bounds__(SF_CH * SF_LANES) void bn_stats_final_kernel(
+    const float* __restrict__ part, long M, int C, int tile_rows, int ntiles,
+    const float* __restrict__ gamma, BnState st, float* pack) {
+  __shared__ float sh[2][SF_LANES][SF_CH];
+  const int cl = threadIdx.x % SF_CH, tl = threadIdx.x / SF_CH;
+  const int c = blockIdx.x * SF_CH + cl;
+  float A = 0.f, B = 0.f, p = 0.f;
+  if (c < C) {
+    const float fr = (float)tile_rows, inv_fr = 1.f / fr;
+    const float2 v0 = *(const float2*)(part + 2 * (size_t)c);
+    p = M < tile_rows ? v0.x / (float)M : v0.x * inv_fr;
+#pragma unroll 4
+    for (int t = tl; t < ntiles; t += SF_LANES) {
+      const float2 v = *(const float2*)(part + 2 * ((size_t)t * C + c));
+      const long rows = M - (long)t * tile_rows;
+      const bool rag = rows < tile_rows;
+      const float n = rag ? (float)rows : fr;
+      const float d = (rag ? v.x / n : v.x * inv_fr) - p;
+      A = __builtin_fmaf(n, d, A);
+      B += __builtin_fmaf(n * d, d, v.y);
+    }
+  }
+  sh[0][tl][cl] = A;
+  sh[1][tl][cl] = B;
+  __syncthreads();
+  if (tl == 0 && c < C) {
+#pragma unroll 8
+    for (int k = 1; k < SF_LANES; ++k) {
+      A += sh[0][k][cl];
+      B += sh[1][k][cl];
+    }
+    const float N = (float)M;
+    const float dm = A / N;
+    const float mean = p + dm;
+    const float var = fmaxf(B / N - dm * dm, 0.f);
+    const float inv = rsqrtf(var + SEG_BN_EPS);
+    st.mean[c] = mean;
+    st.invstd[c] = inv;
+    st.scale[c] = gamma[c] * inv;
+    st.var_unb[c] = var * (N / (N > 1.f ? N - 1.f : 1.f));
+    if (pack) {
+      pack[c] = mean;
+      pack[C + c] = var + mean * mean;
+    }
+  }
+}
+
+// backward finalize: sums of the per-row-block (sum dyhat, sum dyhat*xhat) partials, 32
+// channels x 64 partial lanes per block, fixed order
+__global__ __launch_bounds__(BF_CH * BF_LANES) void bn_bwd_final_kernel(
+    const float* __restrict__ part, int rb, long M, int C, BnState st, float* dgamma,
+    float* dbeta) {
+  __shared__ float sh[2][BF_LANES][BF_CH];
+  const int cl = threadIdx.x % BF_CH, tl = threadIdx.x / BF_CH;
+  const int c = blockIdx.x * BF_CH + cl;
+  float s1 = 0.f, s2 = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = tl; k < rb; k += BF_LANES) {
+      const float2 v = *(const float2*)(part + 2 * ((size_t)k * C + c));
+      s1 += v.x;
+      s2 += v.y;
+    }
+  }
+  sh[0][tl][cl] = s1;
+  sh[1][tl][cl] = s2;
+  __syncthreads();
+  if (tl == 0 && c < C) {
+#pragma unroll 8
+    for (int k = 1; k < BF_LANES; ++k) {
+      s1 += sh[0][k][cl];
+      s2 += sh[1][k][cl];
+    }
+    st.sdy[c] = s1 / (float)M;
+    st.sdyx[c] = s2 / (float)M;
+    if (dgamma) dgamma[c] = s2;
+    if (dbeta) dbeta[c] = s1;
   }
 }
 
@@ -658,11 +746,18 @@ hipError_t launch_bn_stats_finalize(const float* tile_part, long M, int C, int t
                                     float* scratch, const float* gamma, BnState st,
                                     hipStream_t s, float* pack) {
   int ntiles = ceil_div(M, tile_rows);
-  int G = ceil_div(ntiles, STAT_TPB);
-  hipLaunchKernelGGL(bn_stats_stage1, dim3(ceil_div(C, 64), G), dim3(256), 0, s, tile_part, M, C,
-                     tile_rows, ntiles, scratch);
-  hipLaunchKernelGGL(bn_stats_stage2, dim3(ceil_div(C, 64)), dim3(64), 0, s, scratch, G, C, gamma,
-                     st, pack);
+  // A/B: SEG_BN_STATS_2STAGE=1 restores the two-launch Chan merge (stage1 + stage2)
+  static const bool two_stage = getenv("SEG_BN_STATS_2STAGE") && atoi(getenv("SEG_BN_STATS_2STAGE"));
+  if (two_stage) {
+    int G = ceil_div(ntiles, STAT_TPB);
+    hipLaunchKernelGGL(bn_stats_stage1, dim3(ceil_div(C, 64), G), dim3(256), 0, s, tile_part, M, C,
+                       tile_rows, ntiles, scratch);
+    hipLaunchKernelGGL(bn_stats_stage2, dim3(ceil_div(C, 64)), dim3(64), 0, s, scratch, G, C, gamma,
+                       st, pack);
+  } else {
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(ceil_div(C, SF_CH)), dim3(SF_CH * SF_LANES), 0,
+                       s, tile_part, M, C, tile_rows, ntiles, gamma, st, pack);
+  }
   return hipGetLastError();
 }
 
@@ -707,8 +802,13 @@ hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipSt
 
 hipError_t launch_bn_bwd_finalize(const float* part, int rb, long M, int C, BnState st,
                                   float* dgamma, float* dbeta, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 8)), dim3(256), 0, s, part, rb, M,
-                     C, st, dgamma, dbeta);
+  static const int which = getenv("SEG_BN_BWD_FINAL") ? atoi(getenv("SEG_BN_BWD_FINAL")) : 1;
+  if (which == 0)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 8)), dim3(256), 0, s, part, rb, M,
+                       C, st, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ceil_div(C, BF_CH)), dim3(BF_CH * BF_LANES), 0, s,
+                       part, rb, M, C, st, dgamma, dbeta);
   return hipGetLastError();
 }
 

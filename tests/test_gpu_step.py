@@ -95,7 +95,7 @@ def test_train_step_fp32(cuda, cfg):
     assert abs(nat["reg"] - float(L["regularization"])) <= 1e-3 * float(L["regularization"])
     # low-res logits: 1e-3, or 4x the oracle's own fp32-vs-fp64 gap where the network's
     # depth amplifies fp32 rounding beyond that (R101: the fp32 oracle itself is 1.8e-3 off)
-    _, low32, g32, _ = _oracle_step(cfg, params, data, dtype=torch.float32)
+    _, low32, g32, newp32 = _oracle_step(cfg, params, data, dtype=torch.float32)
     c1, c2, c3 = 14, 7, 3
     lg = nat["logits"]
     for key, a, b in (("l1_logits", 0, c1), ("l2_vehicle_logits", c1, c1 + c2),
@@ -116,10 +116,14 @@ def test_train_step_fp32(cuda, cfg):
         wd = cfg.weight_decay if k.endswith("/weights") else 0.0
         exp = w - 0.01 * (nat["grads"][k].astype(np.float64) + wd * w)
         assert _rel(nat["params"][k], exp) < 1e-5, k
-    # BN moving averages of the forward batch statistics (forward quantities: 1e-3)
+    # BN moving averages of the forward batch statistics (forward quantities: 1e-3, or 4x the
+    # fp32 oracle's own gap: a channel mean of a deep layer's output is a cancelling sum, and
+    # R101's depth amplifies fp32 rounding in it past 1e-3)
     for k, v in newp.items():
         if "moving" in k:
-            assert _rel(nat["params"][k], v.detach().numpy().reshape(-1)) < 1e-3, k
+            ref = v.detach().numpy().reshape(-1)
+            gap = _rel(newp32[k].detach().numpy().reshape(-1), ref)
+            assert _rel(nat["params"][k], ref) < max(1e-3, 4 * gap), (k, gap)
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
