@@ -369,15 +369,21 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
   return 0;
 }
 
-int wgrad_splits(const ConvL& L, int ci = 0) {
+// concurrent = the weight gradient runs on the side stream beside the dgrad -> BN chain:
+// target ~128 workgroups (half the CUs, the chain keeps the other half: 90.4 -> 92.9 img/s
+// on C2 against 512, and half the split-K slab traffic); alone (profiled, single stream,
+// seg_op_*): ~2 waves of the 256 CUs. SEG_WGRAD_WGS overrides the concurrent target.
+int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false) {
   if (!ci) ci = L.ci;   // 8 for the tap8 stem
   int BM = L.co_pad <= 64 ? 64 : 128;
   int BN = 128;
   long P = (long)L.N * L.Ho * L.Wo;
   if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, L.k * L.k * ci, P, &BM, &BN);
   long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * ci + BN - 1) / BN);
-  // ~2 waves of 256 single-workgroup CUs, each split >= 32 K-steps of 64 pixels
-  long s = std::max<long>(1, 512 / std::max<long>(tiles, 1));
+  // each split >= 32 K-steps of 64 pixels
+  static const long conc = getenv("SEG_WGRAD_WGS") ? atol(getenv("SEG_WGRAD_WGS")) : 128;
+  const long target = concurrent ? conc : 512;
+  long s = std::max<long>(1, target / std::max<long>(tiles, 1));
   long maxs = std::max<long>(1, P / 2048);
   s = std::min(s, maxs);
   return (int)std::min<long>(s, 256);
@@ -574,7 +580,7 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   a.KH = a.KW = L.k; a.sf = L.stride; a.pad_h = L.pad_h; a.pad_w = L.pad_w; a.dil = L.rate;
   const bool s8 = li == c->stem && c->stem8;
   if (s8) { a.C = 8; a.ldx = 8; }
-  a.splits = wgrad_splits(L, a.C);
+  a.splits = wgrad_splits(L, a.C, c->side_active);
   a.out = c->slab;
   long P = (long)L.N * L.Ho * L.Wo;
   int slot;
@@ -875,7 +881,8 @@ int build(seg_ctx* c) {
     }
     if (seg_half(c->dt)) L.w_lp = (uint16_t*)c->w_lp_flat + L.w_off;   // bf16 or fp16 bits
     const int wci = (&L == &c->convs[c->stem] && c->stem8) ? 8 : L.ci;
-    slab = std::max(slab, (size_t)wgrad_splits(L, wci) * L.co_pad * L.k * L.k * wci);
+    const int sp = std::max(wgrad_splits(L, wci, false), wgrad_splits(L, wci, true));
+    slab = std::max(slab, (size_t)sp * L.co_pad * L.k * L.k * wci);
   }
   if (c->stem8) {
     const ConvL& st = c->convs[c->stem];
