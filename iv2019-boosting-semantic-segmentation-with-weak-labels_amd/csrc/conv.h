@@ -28,6 +28,7 @@ struct ConvArgs {
   float* stats;   // BN partials [mtiles][Co] x {sum, M2} (nullptr = none)
   int tap8;       // 1: C == 8 and every 16-B chunk of K is one tap (the 3-channel stem padded
                   // to 8); K = KH*KW*8 is padded to a multiple of 64 with zero weights
+  int grid_cap;   // persistent launches: workgroups <= grid_cap (0 = one per CU)
 };
 
 struct WgradArgs {

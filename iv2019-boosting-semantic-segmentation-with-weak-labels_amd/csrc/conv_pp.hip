@@ -684,7 +684,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void conv_nt_pp_kernel(ConvArgs a) {
   conv_nt_pp_body<E, ST, PERSIST>(a);
 }
 
-int pp_grid(int nwg) {
+int pp_grid(int nwg, int cap = 0) {
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -694,7 +694,9 @@ int pp_grid(int nwg) {
   }
   const char* e = getenv("SEG_NT_PERSIST");
   if (e && e[0] == '0') return nwg;   // one tile per workgroup (A/B)
-  return nwg < ncu ? nwg : ncu;
+  int g = ncu;
+  if (cap > 0 && cap < g) g = (cap + 7) / 8 * 8;   // keep a multiple of the XCD count
+  return nwg < g ? nwg : g;
 }
 
 template <typename E, int ST, int PERSIST>
@@ -711,7 +713,7 @@ hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
   }
   const long M = (long)a.N * a.Ho * a.Wo;
   const int nwg = ceil_div(M, 256) * ceil_div(a.Co, 256);
-  hipLaunchKernelGGL(kern, dim3(PERSIST ? pp_grid(nwg) : nwg), dim3(PP_THREADS), LDS, s, a);
+  hipLaunchKernelGGL(kern, dim3(PERSIST ? pp_grid(nwg, a.grid_cap) : nwg), dim3(PP_THREADS), LDS, s, a);
   return hipGetLastError();
 }
 

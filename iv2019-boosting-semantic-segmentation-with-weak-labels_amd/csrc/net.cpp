@@ -534,6 +534,9 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
   a.sf = 1; a.st = L.stride;
   a.pad_h = (keff - 1) - L.pad_h; a.pad_w = (keff - 1) - L.pad_w;
   a.dil = L.rate; a.stats = nullptr;
+  // beside a side-stream weight gradient the persistent dgrad takes the CUs that are free
+  static const int dgcap = getenv("SEG_DGRAD_GRID") ? atoi(getenv("SEG_DGRAD_GRID")) : 0;
+  if (c->side_active) a.grid_cap = dgcap;
   long M = (long)L.N * L.H * L.W;
   int slot;
   if (int r = prof_begin(c, S.s, 1, li, 2.0 * M * L.ci * L.k * L.k * L.co * 1e-9 / L.stride / L.stride, &slot)) return r;
