@@ -42,7 +42,6 @@ constexpr int PBK = 64;                    // 16-bit K-elements per K-tile (128-
 constexpr int HALF = 128 * 128;            // one half-tile: 128 rows x 128 B
 constexpr int BUF = 4 * HALF;              // A0 A1 B0 B1
 constexpr int PP_LDS = 2 * BUF;            // 128 KB
-constexpr int EPI_COLS = 64, EPI_LD = EPI_COLS + 4;   // fp32 staging (residual epilogue)
 
 __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
 
@@ -126,9 +125,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
-      // LDS half h = j >> 1, position rr -> tile row. Persistent: wave row rr / 64 owns the
-      // contiguous tile rows [128 * (rr / 64), +128) (quadrant qm = h: rows qm * 64 + 0..63)
-      const int row = PERSIST ? (rr >> 6) * 128 + (j >> 1) * 64 + (rr & 63) : (j >> 1) * 128 + rr;
+      // LDS half h = j >> 1, position rr -> tile row: wave row rr / 64 owns the contiguous
+      // tile rows [128 * (rr / 64), +128) (quadrant qm = h: rows qm * 64 + 0..63)
+      const int row = (rr >> 6) * 128 + (j >> 1) * 64 + (rr & 63);
       a_lc[j] = swz(rr, pc);
       // 32-bit index math (M, N*H*W < 2^31: host check): 64-bit div/rem per row was ~1/3 of
       // the per-tile setup on short-K layers
@@ -240,10 +239,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          // persistent: transposed accumulators (lane = 4 channels of one pixel) for the
-          // register-side statistics and 8-byte staging writes; else the v2 layout
-          acc[qm][qn][i][j] = PERSIST ? Half<E>::mma(bfr[j][s], af[i][s], acc[qm][qn][i][j])
-                                      : Half<E>::mma(af[i][s], bfr[j][s], acc[qm][qn][i][j]);
+          // transposed accumulators (lane = 4 channels of one pixel) for the register-side
+          // statistics and 8-byte staging writes
+          acc[qm][qn][i][j] = Half<E>::mma(bfr[j][s], af[i][s], acc[qm][qn][i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -328,8 +326,8 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     setup_lanes((long)mt_n * BM, nt_n * BN);
     prologue();
   }
-  if constexpr (PERSIST) {
-      // ---- persistent epilogue: transposed accumulators (mfma(B, A)): lane (lq, lr) of
+  {
+      // ---- epilogue: transposed accumulators (mfma(B, A)): lane (lq, lr) of
       // fragment acc[qm][qn][i][j] holds output pixel m = m0 + wm*128 + qm*64 + i*16 + lr and
       // the four channels n = n0 + qn*128 + wn*32 + j*16 + lq*4 + 0..3
     const long mw = m0 + wm * 128;                      // this wave row's 128 contiguous rows
@@ -441,19 +439,57 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     char* const stg = smem + BUF;
     E* Y = (E*)a.y;
     const int s_row = tid >> 4, s_ch = tid & 15;
+    // residuals (dgrad: dx = dgrad + r1 [+ r2]) are added to the fp32 accumulators before the
+    // one rounding, loaded in the accumulator layout (8 B per lane, 8 fragments at a time;
+    // rows past M and channels past Co clamped)
+    const E* R1 = (const E*)a.r;
+    const E* R2 = (const E*)a.r2;
+    // (persistent launches carry no residuals: pp_launch_st routes those to PERSIST = 0, whose
+    // register budget has room for the residual loads)
+    // (PERSIST == 2: persistent with residuals, A/B: the residual loads spill 3 registers)
+    const int nres = PERSIST == 1 ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
+    auto add4 = [](f32x4_t& v, const uint2 u) {
+      const uint32_t w[2] = {u.x, u.y};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint16_t bl = (uint16_t)(w[h] & 0xffffu), bh = (uint16_t)(w[h] >> 16);
+        E lo, hi;
+        __builtin_memcpy(&lo, &bl, 2);
+        __builtin_memcpy(&hi, &bh, 2);
+        v[2 * h] += TypeOps<E>::to_f(lo);
+        v[2 * h + 1] += TypeOps<E>::to_f(hi);
+      }
+    };
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn) {
 #pragma unroll
-      for (int qm = 0; qm < 2; ++qm)
+      for (int qm = 0; qm < 2; ++qm) {
+        uint2 r1v[4][2], r2v[4][2];
+        if (nres) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const long m = mw + qm * 64 + i * 16 + lr;
+              const long mc = m < M ? m : M - 1;
+              const int n = nbase + qn * 128 + j * 16;
+              const int nc = n < a.Co ? n : 0;
+              r1v[i][j] = *(const uint2*)(R1 + (size_t)mc * a.ldr + nc);
+              if (nres == 2) r2v[i][j] = *(const uint2*)(R2 + (size_t)mc * a.ldr2 + nc);
+            }
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int row = wm * 128 + qm * 64 + i * 16 + lr;
             const int ch = wn * 4 + j * 2 + (lq >> 1);
-            *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) =
-                pack4(acc[qm][qn][i][j]);
+            f32x4_t v = acc[qm][qn][i][j];
+            if (nres) add4(v, r1v[i][j]);
+            if (nres == 2) add4(v, r2v[i][j]);
+            *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) = pack4(v);
           }
+      }
       if (a.stats && nvalid > 0) stats_half(qn);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       pp_barrier();
@@ -476,195 +512,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         pp_barrier();
       }
-    }
-  } else {
-    // LDS hand-off inside the epilogue: raw barrier after the LDS writes retire (a
-    // __syncthreads would also wait for the next tile's DMA)
-    auto epi_sync = [&]() {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      pp_barrier();
-    };
-    char* const epi = smem + BUF;
-
-    // ---- epilogue (as conv_nt_v2_kernel): flat fragment view fi' = qm*4 + fi, fj' = qn*2 + fj
-    constexpr int FM = 8, FN = 4, WMW = 2, WM = 128;
-    auto A_ = [&](int fi, int fj) -> f32x4_t& { return acc[fi >> 2][fj >> 1][fi & 3][fj & 1]; };
-    auto row_of = [&](int fi, int k) { return (fi >> 2) * 128 + wm * 64 + (fi & 3) * 16 + lq * 4 + k; };
-    auto col_of = [&](int fj) { return (fj >> 1) * 128 + wn * 32 + (fj & 1) * 16 + lr; };
-    const bool col_writer = lq == 0;
-    const int rows_valid = (int)((M - m0) < BM ? (M - m0) : BM);
-    float* red = (float*)epi;
-    if (a.stats && rows_valid == BM) {
-      float2* red2 = (float2*)epi;
-      constexpr float NL = (float)(4 * FM);
-      float sj[FN], mj[FN];
-  #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        float sm = 0.f, sq = 0.f;
-  #pragma unroll
-        for (int i = 0; i < FM; ++i)
-  #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float x = A_(i, j)[k];
-            sm += x;
-            sq = __builtin_fmaf(x, x, sq);
-          }
-        sj[j] = sm;
-        mj[j] = fmaxf(sq - sm * sm * (1.f / NL), 0.f);
-      }
-      float n = NL;
-  #pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {
-  #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
-          const float d = (s2 - sj[j]) / n;
-          mj[j] = mj[j] + m2 + d * d * (0.5f * n);
-          sj[j] += s2;
-        }
-        n *= 2.f;
-      }
-      if (col_writer)
-  #pragma unroll
-        for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
-      epi_sync();
-      if (wm == 0 && col_writer) {
-  #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int c = col_of(j);
-          float2 t = red2[c];
-          float ntot = (float)WM;
-  #pragma unroll
-          for (int w = 1; w < WMW; ++w) {
-            const float2 u = red2[w * BN + c];
-            const float d = u.x / (float)WM - t.x / ntot;
-            t.y = t.y + u.y + d * d * (ntot * (float)WM / (ntot + (float)WM));
-            t.x += u.x;
-            ntot += (float)WM;
-          }
-          if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = t;
-        }
-      }
-      epi_sync();
-    } else if (a.stats) {
-      float cs[FN];
-  #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        float v = 0.f;
-  #pragma unroll
-        for (int i = 0; i < FM; ++i)
-  #pragma unroll
-          for (int k = 0; k < 4; ++k) v += row_of(i, k) < rows_valid ? A_(i, j)[k] : 0.f;
-  #pragma unroll
-        for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
-        cs[j] = v;
-      }
-      if (col_writer)
-  #pragma unroll
-        for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
-      epi_sync();
-      float mean[FN], tot[FN];
-  #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c = col_of(j);
-        float t = 0.f;
-  #pragma unroll
-        for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
-        tot[j] = t;
-        mean[j] = t / (float)rows_valid;
-      }
-  #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        float v = 0.f;
-  #pragma unroll
-        for (int i = 0; i < FM; ++i)
-  #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float d = A_(i, j)[k] - mean[j];
-            v += row_of(i, k) < rows_valid ? d * d : 0.f;
-          }
-  #pragma unroll
-        for (int o = 16; o <= 32; o <<= 1) v += __shfl_xor(v, o, 64);
-        cs[j] = v;
-      }
-      epi_sync();
-      if (col_writer)
-  #pragma unroll
-        for (int j = 0; j < FN; ++j) red[wm * BN + col_of(j)] = cs[j];
-      epi_sync();
-      if (wm == 0 && col_writer) {
-  #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int c = col_of(j);
-          float t = 0.f;
-  #pragma unroll
-          for (int w = 0; w < WMW; ++w) t += red[w * BN + c];
-          if (n0 + c < a.Co) *(float2*)(a.stats + 2 * ((size_t)mt * a.Co + n0 + c)) = make_float2(tot[j], t);
-        }
-      }
-      epi_sync();
-    }
-    float* stage = (float*)epi;
-    E* Y = (E*)a.y;
-    const E* R1 = (const E*)a.r;
-    const E* R2 = (const E*)a.r2;
-    const int s_rl = tid >> 3, s_cc = tid & 7;
-    // residual operands (dgrad): one pass's rows are loaded into registers before its
-    // accumulators are staged, all loads unconditional (rows past M clamped), so they are in
-    // flight together with the LDS staging and cost one wait per pass (a per-row conditional
-    // load made hipcc wait vmcnt(0) after every load)
-    // (persistent launches carry no residuals: pp_launch_st routes those to PERSIST = 0)
-    const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
-    auto bf8_add = [](float* v, const uint4 u) {
-      float w[8];
-      Half<E>::unpack(u, w);
-  #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] += w[i];
-    };
-  #pragma unroll
-    for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
-      const int cbase = pass * EPI_COLS;
-      const int n = n0 + cbase + s_cc * 8;
-      const int nc = n < a.Co ? n : 0;
-      uint4 r1v[BM / 64], r2v[BM / 64];
-      if (nres) {
-  #pragma unroll
-        for (int rr = 0; rr < BM / 64; ++rr) {
-          const long m = m0 + s_rl + 64 * rr;
-          const long mc = m < M ? m : M - 1;
-          r1v[rr] = *(const uint4*)(R1 + (size_t)mc * a.ldr + nc);
-          if (nres == 2) r2v[rr] = *(const uint4*)(R2 + (size_t)mc * a.ldr2 + nc);
-        }
-      }
-  #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int col = col_of(j);
-        if (col >= cbase && col < cbase + EPI_COLS) {
-  #pragma unroll
-          for (int i = 0; i < FM; ++i)
-  #pragma unroll
-            for (int k = 0; k < 4; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = A_(i, j)[k];
-        }
-      }
-      epi_sync();
-  #pragma unroll
-      for (int rr = 0; rr < BM / 64; ++rr) {
-        const int row = s_rl + 64 * rr;
-        const long m = m0 + row;
-        const float* sp = stage + row * EPI_LD + s_cc * 8;
-        const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
-        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        if (nres) bf8_add(v, r1v[rr]);
-        if (nres == 2) bf8_add(v, r2v[rr]);
-  #ifdef PP_DBG_NOSTORE
-        if (v[0] == 1234.5f)
-  #endif
-        if (n < a.Co && m < M) store8_nt(Y + (size_t)m * a.ldy + n, v);
-      }
-      epi_sync();
-  #ifdef PP_DBG_NOSTAGE
-      break;
-  #endif
     }
   }
   PP_TS(dbg_it, 3);
@@ -701,9 +548,7 @@ int pp_grid(int nwg, int cap = 0) {
 
 template <typename E, int ST, int PERSIST>
 hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
-  // two K-tile buffers; the fp32 staging of the residual (non-persistent) epilogue needs more
-  constexpr int LDS = PERSIST ? PP_LDS : BUF + 256 * EPI_LD * 4;
-  static_assert(LDS >= PP_LDS && LDS <= 160 * 1024, "LDS budget");
+  constexpr int LDS = PP_LDS;   // two K-tile buffers (the epilogue stages through buffer 1)
   auto kern = conv_nt_pp_kernel<E, ST, PERSIST>;
   static bool attr = false;
   if (!attr) {
@@ -719,6 +564,8 @@ hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
 
 template <typename E, int ST>
 hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
+  static const bool pres = getenv("SEG_NT_PERSIST_RES") && atoi(getenv("SEG_NT_PERSIST_RES"));
+  if ((a.r || a.r2) && pres) return pp_launch<E, ST, 2>(a, s);
   if (a.r || a.r2) return pp_launch<E, ST, 0>(a, s);
   return pp_launch<E, ST, 1>(a, s);
 }
