@@ -781,9 +781,10 @@ hipError_t launch_bn_apply(int dtype, int out_f32, const BnApplyArgs& a, hipStre
 }
 
 int bn_bwd_rowblocks(long M, int C) {
-  // ~1024 blocks, each >= 64 rows
+  // ~1024 blocks, each >= 64 rows (SEG_BN_RB: A/B of the cap)
+  static const long cap = getenv("SEG_BN_RB") ? atol(getenv("SEG_BN_RB")) : 1024;
   long rb = (M + 63) / 64;
-  if (rb > 1024) rb = 1024;
+  if (rb > cap) rb = cap;
   (void)C;
   return (int)(rb < 1 ? 1 : rb);
 }
