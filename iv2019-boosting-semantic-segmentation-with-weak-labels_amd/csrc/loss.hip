@@ -11,8 +11,14 @@
 
 namespace {
 
-constexpr int LA = 4;     // owned low-res rows per block
-constexpr int LB = 30;    // owned low-res cols per block
+#ifndef LOSS_LA
+#define LOSS_LA 4
+#endif
+#ifndef LOSS_LB
+#define LOSS_LB 30
+#endif
+constexpr int LA = LOSS_LA;   // owned low-res rows per block
+constexpr int LB = LOSS_LB;   // owned low-res cols per block
 constexpr int THREADS = 256;
 constexpr int GLD = THREADS + 1;   // gbuf row stride
 
