@@ -61,6 +61,7 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
   constexpr int XT = 512;          // per-block x-lerp table (full-res columns of the footprint)
   __shared__ float xlt[XT];        // xl(w)
   __shared__ short xlo_t[XT], xhi_t[XT];
+  __shared__ float wa_t[XT], wb_t[XT];   // x-transpose weights: to column lo / to column hi
   __shared__ float red[6][THREADS / 64];
 
   const int tid = threadIdx.x;
@@ -99,6 +100,8 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
       xlt[w - w_begin] = xl;
       xlo_t[w - w_begin] = (short)lo;
       xhi_t[w - w_begin] = (short)hi;
+      wa_t[w - w_begin] = hi == lo ? 1.f : 1.f - xl;   // clamped last column takes both shares
+      wb_t[w - w_begin] = xl;
     }
     __syncthreads();
   }
@@ -294,6 +297,15 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
             float sacc = 0.f;
             // w with lo == j  -> weight (1 - xl) [+ xl if j is the clamped last column]
             int wa = max(wstart[jj + 1], wc), wb = min(wstart[jj + 2], cend);
+            if (use_xt) {
+              // precomputed weights: one gbuf read + one broadcast table read per w
+              for (int w = wa; w < wb; ++w) sacc += gbuf[c * GLD + (w - wc)] * wa_t[w - w_begin];
+              wa = max(wstart[jj], wc);
+              wb = min(wstart[jj + 1], cend);
+              for (int w = wa; w < wb; ++w) sacc += gbuf[c * GLD + (w - wc)] * wb_t[w - w_begin];
+              rowacc[u] += sacc;
+              continue;
+            }
             for (int w = wa; w < wb; ++w) {
               int lo, hi;
               float xl;
