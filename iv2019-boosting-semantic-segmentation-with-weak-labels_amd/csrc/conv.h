@@ -47,8 +47,10 @@ hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t
 hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s);
 hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride, long n,
                                 float* out, int accumulate, hipStream_t s);
-// all layers' flips in one launch: table of FlipJob (device), prefix = first output element
+// all layers' flips in one launch: table of FlipJob (device), prefix = the job's first tile;
+// total = flip tiles over all jobs
 struct FlipJob { const void* w; void* wt; int co, k, ci; long prefix; };
+long flip_tiles(int co, int k, int ci);
 hipError_t launch_weight_flip_batched(int dtype, const FlipJob* jobs, int njobs, long total,
                                       hipStream_t s);
 hipError_t launch_weight_flip_transpose(int dtype, const void* w, void* wt, int co, int kh, int kw,

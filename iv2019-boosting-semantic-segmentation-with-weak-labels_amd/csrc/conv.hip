@@ -555,23 +555,39 @@ __global__ void weight_flip_transpose_kernel(const T* __restrict__ w, T* __restr
   wt[i] = w[(((size_t)o * kh + (kh - 1 - y)) * kw + (kw - 1 - x)) * ci + c];
 }
 
+// every layer's dgrad weight flip [co][k][k][ci] -> [ci][k][k][co] (taps reversed) in one
+// launch: one block per 64 x 64 (co x ci) tile of one tap of one layer, transposed through
+// LDS so both the reads (ci) and the writes (co) are contiguous; FlipJob.prefix = the layer's
+// first tile (the per-element version with a per-element job search and 64-bit div/mod took
+// 205 us per step)
 template <typename T>
-__global__ void weight_flip_batched_kernel(const FlipJob* __restrict__ jobs, int njobs, long total) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int lo = 0, hi = njobs - 1;   // last job with prefix <= i
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (jobs[mid].prefix <= i) lo = mid; else hi = mid - 1;
-    }
-    const FlipJob J = jobs[lo];
-    const long r = i - J.prefix;   // index over [ci][k][k][co]
-    const int o = (int)(r % J.co);
-    long t = r / J.co;
-    const int x = (int)(t % J.k);
-    t /= J.k;
-    const int y = (int)(t % J.k);
-    const int c = (int)(t / J.k);
-    ((T*)J.wt)[r] = ((const T*)J.w)[(((size_t)o * J.k + (J.k - 1 - y)) * J.k + (J.k - 1 - x)) * J.ci + c];
+__global__ __launch_bounds__(256) void weight_flip_tiled_kernel(const FlipJob* __restrict__ jobs, int njobs) {
+  __shared__ T tile[64][65];
+  const long b = blockIdx.x;
+  int lo = 0, hi = njobs - 1;   // last job with prefix <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].prefix <= b) lo = mid; else hi = mid - 1;
+  }
+  const FlipJob J = jobs[lo];
+  const int tl = (int)(b - J.prefix);
+  const int tco = (J.co + 63) / 64, tci = (J.ci + 63) / 64;
+  const int tap = tl / (tco * tci), rem = tl - tap * (tco * tci);
+  const int o0 = (rem / tci) * 64, c0 = (rem % tci) * 64;
+  const int y = tap / J.k, x = tap - y * J.k;
+  const int sy = J.k - 1 - y, sx = J.k - 1 - x;
+  const T* W = (const T*)J.w;
+  T* WT = (T*)J.wt;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int r = e >> 6, cc = e & 63;   // r: output channel, cc: input channel
+    const int o = o0 + r, ci = c0 + cc;
+    if (o < J.co && ci < J.ci) tile[r][cc] = W[(((size_t)o * J.k + sy) * J.k + sx) * J.ci + ci];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int r = e >> 6, cc = e & 63;   // r: input channel, cc: output channel
+    const int ci = c0 + r, o = o0 + cc;
+    if (o < J.co && ci < J.ci) WT[(((size_t)ci * J.k + y) * J.k + x) * J.co + o] = tile[cc][r];
   }
 }
 
@@ -718,12 +734,11 @@ hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride
 
 hipError_t launch_weight_flip_batched(int dtype, const FlipJob* jobs, int njobs, long total,
                                       hipStream_t s) {
-  long g = (total + 255) / 256;
-  if (g > 8192) g = 8192;
+  // total = number of 64 x 64 tiles over all jobs (flip_tiles)
   if (seg_half(dtype))   // a bit copy: one 16-bit instantiation serves bf16 and fp16
-    hipLaunchKernelGGL(weight_flip_batched_kernel<bf16_t>, dim3((int)g), dim3(256), 0, s, jobs, njobs, total);
+    hipLaunchKernelGGL(weight_flip_tiled_kernel<bf16_t>, dim3((int)total), dim3(256), 0, s, jobs, njobs);
   else
-    hipLaunchKernelGGL(weight_flip_batched_kernel<float>, dim3((int)g), dim3(256), 0, s, jobs, njobs, total);
+    hipLaunchKernelGGL(weight_flip_tiled_kernel<float>, dim3((int)total), dim3(256), 0, s, jobs, njobs);
   return hipGetLastError();
 }
 
@@ -738,4 +753,8 @@ hipError_t launch_weight_flip_transpose(int dtype, const void* w, void* wt, int 
     hipLaunchKernelGGL(weight_flip_transpose_kernel<float>, g, dim3(256), 0, s, (const float*)w,
                        (float*)wt, co, kh, kw, ci);
   return hipGetLastError();
+}
+
+long flip_tiles(int co, int k, int ci) {
+  return (long)k * k * ((co + 63) / 64) * ((ci + 63) / 64);
 }

@@ -1202,7 +1202,7 @@ int seg_bind_buffers(seg_ctx* c, float* params, float* grads, float* momentum, f
   for (auto& L : c->convs)
     if (L.wt_lp) {
       jobs.push_back({L.w_lp, L.wt_lp, L.co, L.k, L.ci, tot});
-      tot += (long)L.co * L.k * L.k * L.ci;
+      tot += flip_tiles(L.co, L.k, L.ci);
     }
   c->n_flip = (int)jobs.size();
   c->flip_total = tot;
