@@ -17,3 +17,8 @@ t(lambda: c.copy_(a), 4 * n, "copy 1R1W")
 t(lambda: torch.add(a, b, out=c), 6 * n, "add 2R1W")
 t(lambda: a.view(-1, 2048).sum(0, dtype=torch.float32), 2 * n, "colsum 1R")
 t(lambda: c.zero_(), 2 * n, "fill 1W")
+# the C2 BN layer sizes (67 MB / 268 MB per operand): short streams pay launch ramp and tail
+for m in (131072 * 256, 131072 * 1024):
+    x = torch.randn(m, dtype=torch.bfloat16, device="cuda")
+    y = torch.empty_like(x)
+    t(lambda: y.copy_(x), 4 * m, f"copy 1R1W {m * 2 >> 20} MB")
