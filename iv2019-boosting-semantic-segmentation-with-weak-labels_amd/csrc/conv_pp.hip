@@ -465,6 +465,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
         uint2 r1v[4][2], r2v[4][2];
+        uint32_t mkv[4][2];
         if (nres) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -476,6 +477,8 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
               const int nc = n < a.Co ? n : 0;
               r1v[i][j] = *(const uint2*)(R1 + (size_t)mc * a.ldr + nc);
               if (nres == 2) r2v[i][j] = *(const uint2*)(R2 + (size_t)mc * a.ldr2 + nc);
+              if (a.rmask)   // the 4 ReLU bits of these channels: a nibble of the mask byte
+                mkv[i][j] = a.rmask[(size_t)mc * a.ldm + (nc >> 3)] >> (nc & 4);
             }
         }
 #pragma unroll
@@ -485,7 +488,17 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             const int row = wm * 128 + qm * 64 + i * 16 + lr;
             const int ch = wn * 4 + j * 2 + (lq >> 1);
             f32x4_t v = acc[qm][qn][i][j];
-            if (nres) add4(v, r1v[i][j]);
+            if (nres) {
+              if (a.rmask) {   // r1 = the gradient above a ReLU: masked here (no dyhat tensor)
+                const uint32_t mk = mkv[i][j];
+                uint2 u = r1v[i][j];
+                u.x &= ((mk & 1u) ? 0x0000ffffu : 0u) | ((mk & 2u) ? 0xffff0000u : 0u);
+                u.y &= ((mk & 4u) ? 0x0000ffffu : 0u) | ((mk & 8u) ? 0xffff0000u : 0u);
+                add4(v, u);
+              } else {
+                add4(v, r1v[i][j]);
+              }
+            }
             if (nres == 2) add4(v, r2v[i][j]);
             *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) = pack4(v);
           }
@@ -571,6 +584,11 @@ hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+bool conv_nt_takes_rmask(int dtype, const ConvArgs& a) {
+  return seg_half(dtype) && a.Co > 128 && conv_nt_uses_v2(dtype, 0, a) && conv_nt_pp_enabled() &&
+         conv_nt_pp_ok(a);
+}
 
 // ping-pong config: the v2 fast-path preconditions (conv_nt_v2_ok, no tap8), Co > 128 and an
 // operands of < 2^31 bytes (32-bit buffer offsets), kernels up to 4 x 4 (tap validity bits)
