@@ -18,12 +18,16 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W,
   const long total = (long)N * Ho * Wo * cg_n;
   for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
        it += (long)gridDim.x * blockDim.x) {
-    int cg = (int)(it % cg_n);
-    long p = it / cg_n;
-    int wo = (int)(p % Wo);
-    long t = p / Wo;
-    int ho = (int)(t % Ho);
-    int n = (int)(t / Ho);
+    // 32-bit index decode (launch_* checks the item count < 2^31): 64-bit div/mod per
+    // element was most of these streaming kernels' time
+    const unsigned ui = (unsigned)it, up = ui / (unsigned)cg_n;
+    const int cg = (int)(ui - up * (unsigned)cg_n);
+    const long p = up;
+    const unsigned ut = up / (unsigned)Wo;
+    const int wo = (int)(up - ut * (unsigned)Wo);
+    const unsigned un = ut / (unsigned)Ho;
+    const int ho = (int)(ut - un * (unsigned)Ho);
+    const int n = (int)un;
     float mx[8];
     uint32_t am[8];
 #pragma unroll
@@ -59,12 +63,15 @@ __global__ void maxpool_bwd_kernel(const uint8_t* __restrict__ arg, int N, int H
   const long total = (long)N * H * W * cg_n;
   for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
        it += (long)gridDim.x * blockDim.x) {
-    int cg = (int)(it % cg_n);
-    long p = it / cg_n;
-    int wi = (int)(p % W);
-    long t = p / W;
-    int hi = (int)(t % H);
-    int n = (int)(t / H);
+    // 32-bit index decode (launch_* checks the item count < 2^31): 64-bit div/mod per
+    // element was most of these streaming kernels' time
+    const unsigned ui = (unsigned)it, up = ui / (unsigned)cg_n;
+    const int cg = (int)(ui - up * (unsigned)cg_n);
+    const unsigned ut = up / (unsigned)W;
+    const int wi = (int)(up - ut * (unsigned)W);
+    const unsigned un = ut / (unsigned)H;
+    const int hi = (int)(ut - un * (unsigned)H);
+    const int n = (int)un;
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = 0.f;
@@ -103,12 +110,16 @@ __global__ void add_strided_kernel(T* __restrict__ dx, int H, int W, int lddx, c
   const long total = (long)N * Ho * Wo * cg_n;
   for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
        it += (long)gridDim.x * blockDim.x) {
-    int cg = (int)(it % cg_n);
-    long p = it / cg_n;
-    int wo = (int)(p % Wo);
-    long t = p / Wo;
-    int ho = (int)(t % Ho);
-    int n = (int)(t / Ho);
+    // 32-bit index decode (launch_* checks the item count < 2^31): 64-bit div/mod per
+    // element was most of these streaming kernels' time
+    const unsigned ui = (unsigned)it, up = ui / (unsigned)cg_n;
+    const int cg = (int)(ui - up * (unsigned)cg_n);
+    const long p = up;
+    const unsigned ut = up / (unsigned)Wo;
+    const int wo = (int)(up - ut * (unsigned)Wo);
+    const unsigned un = ut / (unsigned)Ho;
+    const int ho = (int)(ut - un * (unsigned)Ho);
+    const int n = (int)un;
     T* d = dx + ((size_t)((long)n * H + ho * s) * W + wo * s) * lddx + cg * 8;
     float a[8], b[8];
     Vec8<T>::load(d, a);
@@ -260,12 +271,16 @@ __global__ void resize_fwd_kernel(const T* __restrict__ x, int N, int hi_n, int 
   const long total = (long)N * Ho * Wo * cg_n;
   for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
        it += (long)gridDim.x * blockDim.x) {
-    int cg = (int)(it % cg_n);
-    long p = it / cg_n;
-    int wo = (int)(p % Wo);
-    long t = p / Wo;
-    int ho = (int)(t % Ho);
-    int n = (int)(t / Ho);
+    // 32-bit index decode (launch_* checks the item count < 2^31): 64-bit div/mod per
+    // element was most of these streaming kernels' time
+    const unsigned ui = (unsigned)it, up = ui / (unsigned)cg_n;
+    const int cg = (int)(ui - up * (unsigned)cg_n);
+    const long p = up;
+    const unsigned ut = up / (unsigned)Wo;
+    const int wo = (int)(up - ut * (unsigned)Wo);
+    const unsigned un = ut / (unsigned)Ho;
+    const int ho = (int)(ut - un * (unsigned)Ho);
+    const int n = (int)un;
     int y0, y1, x0, x1;
     float yl, xl;
     tf_lerp(ho, hi_n, Ho, y0, y1, yl);
@@ -295,12 +310,16 @@ __global__ void psp_input_bwd_kernel(const T* __restrict__ dcat, int ldcat, Grid
   const long total = (long)N * H * W * cg_n;
   for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
        it += (long)gridDim.x * blockDim.x) {
-    int cg = (int)(it % cg_n);
-    long p = it / cg_n;
-    int w = (int)(p % W);
-    long t = p / W;
-    int h = (int)(t % H);
-    int n = (int)(t / H);
+    // 32-bit index decode (launch_* checks the item count < 2^31): 64-bit div/mod per
+    // element was most of these streaming kernels' time
+    const unsigned ui = (unsigned)it, up = ui / (unsigned)cg_n;
+    const int cg = (int)(ui - up * (unsigned)cg_n);
+    const long p = up;
+    const unsigned ut = up / (unsigned)W;
+    const int w = (int)(up - ut * (unsigned)W);
+    const unsigned un = ut / (unsigned)H;
+    const int h = (int)(ut - un * (unsigned)H);
+    const int n = (int)un;
     float a[8];
     Vec8<T>::load(dcat + (size_t)p * ldcat + cg * 8, a);
     for (int gi = 0; gi < g.n; ++gi) {
@@ -324,6 +343,7 @@ hipError_t launch_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int
                               void* y, int Ho, int Wo, int ldy, int pad_h, int pad_w, void* arg,
                               hipStream_t s) {
   if (C % 8 || ldx % 8 || ldy % 8) return hipErrorInvalidValue;
+  if ((long)N * Ho * Wo * C / 8 >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit decode
   dim3 g(grid_for((long)N * Ho * Wo * C / 8));
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, N, H, W, C,
@@ -341,6 +361,7 @@ hipError_t launch_maxpool_bwd(int dtype, const void* arg, int N, int H, int W, i
                               const void* dy, int Ho, int Wo, int lddy, void* dx, int lddx,
                               int pad_h, int pad_w, hipStream_t s) {
   if (C % 8 || lddy % 8 || lddx % 8) return hipErrorInvalidValue;
+  if ((long)N * H * W * C / 8 >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit decode
   dim3 g(grid_for((long)N * H * W * C / 8));
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, N, H, W,
@@ -357,6 +378,7 @@ hipError_t launch_maxpool_bwd(int dtype, const void* arg, int N, int H, int W, i
 hipError_t launch_add_strided(int dtype, void* dx, int H, int W, int lddx, const void* g, int N,
                               int Ho, int Wo, int C, int ldg, int stride, hipStream_t s) {
   if (C % 8 || lddx % 8 || ldg % 8) return hipErrorInvalidValue;
+  if ((long)N * Ho * Wo * C / 8 >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit decode
   dim3 gr(grid_for((long)N * Ho * Wo * C / 8));
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(add_strided_kernel<bf16_t>, gr, dim3(256), 0, s, (bf16_t*)dx, H, W, lddx,
@@ -416,6 +438,7 @@ hipError_t launch_grid_colreduce(int dtype, const float* part, int N, int H, int
 hipError_t launch_resize_fwd(int dtype, const void* x, int N, int hi, int wi, int C, int ldx,
                              void* y, int Ho, int Wo, int ldy, hipStream_t s) {
   if (C % 8 || ldx % 8 || ldy % 8) return hipErrorInvalidValue;
+  if ((long)N * Ho * Wo * C / 8 >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit decode
   dim3 gr(grid_for((long)N * Ho * Wo * C / 8));
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(resize_fwd_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)x, N, hi, wi,
@@ -435,6 +458,7 @@ hipError_t launch_psp_input_bwd(int dtype, const void* dcat, int ldcat, const Gr
   if (C % 8 || ldcat % 8 || lddx % 8) return hipErrorInvalidValue;
   InPtrs ip;
   for (int i = 0; i < SEG_MAX_GRIDS; ++i) ip.p[i] = i < g.n ? dpooled[i] : nullptr;
+  if ((long)N * H * W * C / 8 >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit decode
   dim3 gr(grid_for((long)N * H * W * C / 8));
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(psp_input_bwd_kernel<bf16_t>, gr, dim3(256), 0, s, (const bf16_t*)dcat, ldcat,
