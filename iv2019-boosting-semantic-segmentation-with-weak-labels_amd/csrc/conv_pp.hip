@@ -790,7 +790,9 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
     __builtin_memcpy(&f0, &v0, 16);
     __builtin_memcpy(&f1, &v1, 16);
   };
-  V af[4][2], bfr[2][2];
+  // both B quadrants stay in registers for the K-tile (phase 3 reuses B0 from phase 0: one
+  // LDS read burst in three fewer per K-tile)
+  V af[4][2], bfq[2][2][2];   // bfq[qn][frag][k-substep]
   auto read_a = [&](int kb, int qm) {
     const uint32_t off = smem_lds + (kb & 1) * WBUF + qm * WHALF;
 #pragma unroll
@@ -799,7 +801,7 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
   auto read_b = [&](int kb, int qn) {
     const uint32_t off = smem_lds + (kb & 1) * WBUF + (2 + qn) * WHALF;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) frag2(off + b_rb[j], bfr[j][0], bfr[j][1]);
+    for (int j = 0; j < 2; ++j) frag2(off + b_rb[j], bfq[qn][j][0], bfq[qn][j][1]);
   };
   auto mfma_q = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm fragment reads
@@ -813,7 +815,7 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfr[j][s], acc[qm][qn][i][j]);
+          acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfq[qn][j][s], acc[qm][qn][i][j]);
 #ifdef PP_WG_DYNPRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -860,8 +862,7 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       pp_barrier();
       mfma_q(1, 1);
       pp_barrier();
-      read_b(kb, 0);
-      if (more) issue_half(kb + 1, 1);
+      if (more) issue_half(kb + 1, 1);   // B0 is still in registers from phase 0
       if (more && wm == 1) wait_next(true);
       pp_barrier();
       mfma_q(1, 0);
