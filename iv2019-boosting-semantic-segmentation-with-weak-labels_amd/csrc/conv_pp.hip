@@ -212,7 +212,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 
   f32x4_t acc[2][2][4][2];   // [qm][qn][fi][fj]
 
-  V af[4][2], bfr[2][2];   // [frag][k-half]
+  V af[4][2], bfq[2][2][2];   // [frag][k-half]; B per quadrant qn: B0 kept for phase 3
   auto read_a = [&](const char* buf, int qm) {
     const char* A = buf + qm * HALF;
 #pragma unroll
@@ -228,7 +228,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     for (int j = 0; j < 2; ++j) {
       const int row = wn * 32 + j * 16 + lr;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) bfr[j][s] = *(const V*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
+      for (int s = 0; s < 2; ++s) bfq[qn][j][s] = *(const V*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
     }
   };
   auto mfma_q = [&](int qm, int qn) {
@@ -241,7 +241,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         for (int j = 0; j < 2; ++j)
           // transposed accumulators (lane = 4 channels of one pixel) for the register-side
           // statistics and 8-byte staging writes
-          acc[qm][qn][i][j] = Half<E>::mma(bfr[j][s], af[i][s], acc[qm][qn][i][j]);
+          acc[qm][qn][i][j] = Half<E>::mma(bfq[qn][j][s], af[i][s], acc[qm][qn][i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -306,8 +306,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     pp_barrier();
     mfma_q(1, 1);
     pp_barrier();
-    // phase 3: quadrant (1,0), needs B0; refill A1
-    read_b(buf, 0);
+    // phase 3: quadrant (1,0), B0 still in registers from phase 0; refill A1
     if (more) issue_half(kb + 1, tn, 1);
     if (more && wm == 1) wait_next(true);
     pp_barrier();
