@@ -594,7 +594,10 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   a.KH = a.KW = L.k; a.sf = L.stride; a.pad_h = L.pad_h; a.pad_w = L.pad_w; a.dil = L.rate;
   const bool s8 = li == c->stem && c->stem8;
   if (s8) { a.C = 8; a.ldx = 8; }
-  a.splits = wgrad_splits(L, a.C, c->side_active);
+  // the stem's weight gradient is the last work of the step (its dgrad is skipped): nothing
+  // runs beside it, so it takes the whole chip (tools/timeline.py: the compute stream idled
+  // ~0.75 ms waiting for it)
+  a.splits = wgrad_splits(L, a.C, c->side_active && li != c->stem);
   a.out = c->slab;
   long P = (long)L.N * L.Ho * L.Wo;
   int slot;
