@@ -663,17 +663,33 @@ __global__ void stem_pad_weights_kernel(const bf16_t* __restrict__ w, bf16_t* __
   const int t = k >> 3, c = k & 7;
   wp[i] = (t < taps && c < ci) ? w[((size_t)o * taps + t) * ci + c] : (bf16_t)0;
 }
-__global__ void splitk_reduce_pad8_kernel(const float* __restrict__ part, int splits, long stride,
-                                          int co, int taps, int ci, float* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// stem weight gradient: few outputs (co * 49 * 3) over many splits, so 8 lanes per output
+// each sum every 8th split, then a fixed-order tree over the lanes (one serial loop per
+// output over 256 splits took 82 us)
+constexpr int RP8_OUT = 32, RP8_LANES = 8;
+__global__ __launch_bounds__(RP8_OUT * RP8_LANES) void splitk_reduce_pad8_kernel(
+    const float* __restrict__ part, int splits, long stride, int co, int taps, int ci,
+    float* __restrict__ out) {
+  __shared__ float sh[RP8_LANES][RP8_OUT];
+  const int ol = threadIdx.x % RP8_OUT, zl = threadIdx.x / RP8_OUT;
+  const int i = blockIdx.x * RP8_OUT + ol;
   const int n = co * taps * ci;
-  if (i >= n) return;
-  const int o = i / (taps * ci), r = i - o * taps * ci;
-  const int t = r / ci, c = r - t * ci;
-  const long src = (long)o * taps * 8 + t * 8 + c;
   float acc = 0.f;
-  for (int z = 0; z < splits; ++z) acc += part[(size_t)z * stride + src];   // fixed order
-  out[i] = acc;
+  if (i < n) {
+    const int o = i / (taps * ci), r = i - o * taps * ci;
+    const int t = r / ci, c = r - t * ci;
+    const long src = (long)o * taps * 8 + t * 8 + c;
+#pragma unroll 4
+    for (int z = zl; z < splits; z += RP8_LANES) acc += part[(size_t)z * stride + src];
+  }
+  sh[zl][ol] = acc;
+  __syncthreads();
+  if (zl == 0 && i < n) {
+    float v = sh[0][ol];
+#pragma unroll
+    for (int k = 1; k < RP8_LANES; ++k) v += sh[k][ol];
+    out[i] = v;
+  }
 }
 }  // namespace
 
@@ -695,8 +711,8 @@ hipError_t launch_stem_pad_weights(const bf16_t* w, bf16_t* wp, int co, int taps
 }
 hipError_t launch_splitk_reduce_pad8(const float* part, int splits, long split_stride, int co,
                                      int taps, int ci, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(splitk_reduce_pad8_kernel, dim3(ceil_div((long)co * taps * ci, 256)), dim3(256), 0,
-                     s, part, splits, split_stride, co, taps, ci, out);
+  hipLaunchKernelGGL(splitk_reduce_pad8_kernel, dim3(ceil_div((long)co * taps * ci, RP8_OUT)),
+                     dim3(RP8_OUT * RP8_LANES), 0, s, part, splits, split_stride, co, taps, ci, out);
   return hipGetLastError();
 }
 
