@@ -102,6 +102,19 @@ int seg_outputs(seg_ctx* ctx, const float** losses, const float** reg,
 int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions, int64_t n,
                   int num_classes, int32_t* cm, void* stream);
 
+/* EVAL / PREDICT (define_estimator_hierarchical.py:161-232) ------------------------------
+ * seg_set_bn_inference(ctx, 1): later seg_forward calls normalise with the moving statistics
+ * (tf.contrib.layers.batch_norm is_training = batch_norm_accumulate_statistics = False,
+ * models/resnet50_extended_model_hierarchical.py:40-49,306-307); 0 restores training BN.
+ * seg_predict: decisions of the last seg_forward at out_h x out_w: fused hierarchical argmax
+ * (hierarchical.py:88-130) -> cid_map[n_map] (training -> evaluation/inference cids, -1 =
+ * void -> max+1; _map_predictions_to_new_cids :490-522) -> optional _replace_voids
+ * (:577-630) -> NEAREST_NEIGHBOR align_corners resize to out_h x out_w (_resize_predictions
+ * :524-575). decisions_out: device int32 [N][out_h][out_w]. */
+int seg_set_bn_inference(seg_ctx* ctx, int on);
+int seg_predict(seg_ctx* ctx, const int32_t* cid_map, int n_map, int replace_voids, int out_h,
+                int out_w, int32_t* decisions_out, void* stream);
+
 /* loss scaling (fp16 storage, BASELINE config C5: fp16 with fp32 master gradients). The
  * gradient seed of seg_loss is multiplied by `scale`; seg_apply_update first flags non-finite
  * weight/BN gradients (device int, seg_found_inf), unscales them by grad_scale / scale (the BN

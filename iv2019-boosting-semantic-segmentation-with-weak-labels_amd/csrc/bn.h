@@ -53,6 +53,9 @@ hipError_t launch_bn_stats_finalize(const float* tile_part, long M, int C, int t
 // cross-replica BN: the replica-summed pack -> global mean / biased variance in st
 hipError_t launch_bn_sync_unpack(const float* pack, int C, float inv_world, const float* gamma,
                                  BnState st, hipStream_t s);
+// inference mode: st from the moving statistics (no batch statistics)
+hipError_t launch_bn_infer_finalize(const float* mov_mean, const float* mov_var, int C,
+                                    const float* gamma, BnState st, hipStream_t s);
 hipError_t launch_bn_apply(int dtype, int out_f32, const BnApplyArgs& a, hipStream_t s);
 int bn_bwd_rowblocks(long M, int C);
 hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipStream_t s);

@@ -178,6 +178,21 @@ __global__ void bn_sync_unpack_kernel(const float* __restrict__ pack, int C, flo
   st.var_unb[c] = var;
 }
 
+// inference-mode BN (tf.contrib.layers.batch_norm is_training=False, i.e.
+// batch_norm_accumulate_statistics unset; hierarchical.py:306-307): the moving statistics
+// take the place of the batch statistics in the same apply kernel
+__global__ void bn_infer_finalize_kernel(const float* __restrict__ mov_mean,
+                                         const float* __restrict__ mov_var, int C,
+                                         const float* gamma, BnState st) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = rsqrtf(mov_var[c] + SEG_BN_EPS);
+  st.mean[c] = mov_mean[c];
+  st.invstd[c] = inv;
+  st.scale[c] = gamma[c] * inv;
+  st.var_unb[c] = mov_var[c];
+}
+
 // ---- forward apply ---------------------------------------------------------------------
 template <typename T, typename TO, int VEC>
 __global__ void bn_apply_kernel(BnApplyArgs a) {
@@ -765,6 +780,13 @@ hipError_t launch_bn_sync_unpack(const float* pack, int C, float inv_world, cons
                                  BnState st, hipStream_t s) {
   hipLaunchKernelGGL(bn_sync_unpack_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, s, pack, C,
                      inv_world, gamma, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_infer_finalize(const float* mov_mean, const float* mov_var, int C,
+                                    const float* gamma, BnState st, hipStream_t s) {
+  hipLaunchKernelGGL(bn_infer_finalize_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, s, mov_mean,
+                     mov_var, C, gamma, st);
   return hipGetLastError();
 }
 

@@ -33,7 +33,25 @@ struct LossArgs {
   int* l1_decisions;       // optional [N][H][W]
 };
 
+// EVAL / PREDICT decisions (define_estimator_hierarchical.py:161-194,215-232): per output
+// pixel, the NEAREST_NEIGHBOR align_corners source pixel of the network-resolution decision
+// map (_resize_predictions :524-575), recomputed from the low-res logits exactly as the loss
+// head does (bilinear, softmax, argmax, hierarchical fusion), mapped through the training ->
+// evaluation/inference cid table (_map_predictions_to_new_cids :490-522) and, optionally,
+// void decisions replaced by the l1 top-k rule (_replace_voids :577-630).
+struct EvalArgs {
+  const float* logits;     // [N][Hl][Wl][ldl]
+  int N, Hl, Wl, ldl;
+  int H, W;                // network resolution (where decisions are formed)
+  int Ho, Wo;              // output (label) resolution
+  int replace_voids;
+  int n_map;               // entries of map (= training classes)
+  int map[SEG_MAX_PP];     // training cid -> new cid (voids already replaced)
+  int* out;                // [N][Ho][Wo]
+};
+
 int loss_head_blocks(int N, int Hl, int Wl);
+hipError_t launch_eval_decisions(const EvalArgs& a, const LossTables& t, hipStream_t s);
 hipError_t launch_loss_head(const LossArgs& a, const LossTables& t, hipStream_t s);
 // out[0..9] = {seg, l1, l2v, l2h, n1, n2v, n2h, f1, f2v, f2h}; dzscale[ldl] per-channel
 // factors (1/n1 | 0.1/n2v | 0.1/n2h; 0 where the count is 0)

@@ -424,6 +424,91 @@ __global__ void confusion_kernel(const int* __restrict__ lab, const int* __restr
     if (h[i]) atomicAdd(&cm[i], h[i]);
 }
 
+
+// TF 1.12 ResizeNearestNeighbor(align_corners=True) source index (legacy scaler, roundf)
+__device__ __forceinline__ int nn_src(int o, int n_in, int n_out) {
+  const float scale = n_out > 1 ? (float)(n_in - 1) / (float)(n_out - 1) : (float)n_in / (float)n_out;
+  const int i = (int)roundf((float)o * scale);
+  return i < n_in - 1 ? i : n_in - 1;
+}
+
+// one thread per output pixel; the 4 source cells of the bilinear footprint are read from
+// HBM/L2 directly (eval is one forward per batch: this kernel is ~0.1 % of it)
+template <int C1, int C2, int C3>
+__global__ __launch_bounds__(256) void eval_decisions_kernel(EvalArgs a, LossTables t) {
+  constexpr int CT = C1 + C2 + C3;
+  const long total = (long)a.N * a.Ho * a.Wo;
+  for (long id = (long)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+       id += (long)gridDim.x * blockDim.x) {
+    const int xo = (int)(id % a.Wo);
+    const int yo = (int)((id / a.Wo) % a.Ho);
+    const int n = (int)(id / ((long)a.Wo * a.Ho));
+    const int h = nn_src(yo, a.H, a.Ho), w = nn_src(xo, a.W, a.Wo);
+    int ylo, yhi, xlo, xhi;
+    float yl, xl;
+    lerp_of(h, a.Hl, a.H, ylo, yhi, yl);
+    lerp_of(w, a.Wl, a.W, xlo, xhi, xl);
+    const float* base = a.logits + (size_t)n * a.Hl * a.Wl * a.ldl;
+    const float* tl = base + ((size_t)ylo * a.Wl + xlo) * a.ldl;
+    const float* tr = base + ((size_t)ylo * a.Wl + xhi) * a.ldl;
+    const float* bl = base + ((size_t)yhi * a.Wl + xlo) * a.ldl;
+    const float* br = base + ((size_t)yhi * a.Wl + xhi) * a.ldl;
+    float p[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      float top = tl[c] + (tr[c] - tl[c]) * xl;
+      float bot = bl[c] + (br[c] - bl[c]) * xl;
+      p[c] = top + (bot - top) * yl;
+    }
+    // softmax per head (the same arithmetic as the loss head), argmax first max
+    auto softmax = [&](int c0, int nc) {
+      float m = p[c0];
+#pragma unroll
+      for (int c = 1; c < nc; ++c) m = fmaxf(m, p[c0 + c]);
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < nc; ++c) { p[c0 + c] = __expf(p[c0 + c] - m); s += p[c0 + c]; }
+      const float rs = 1.f / s;
+#pragma unroll
+      for (int c = 0; c < nc; ++c) p[c0 + c] = p[c0 + c] * rs;
+    };
+    softmax(0, C1);
+    softmax(C1, C2);
+    softmax(C1 + C2, C3);
+    int d1 = 0;
+    float b1 = p[0];
+#pragma unroll
+    for (int c = 1; c < C1; ++c) if (p[c] > b1) { b1 = p[c]; d1 = c; }
+    int d;
+    if (d1 == t.cid_l1_vehicle) {
+      int b = 0;
+      float bv = p[C1];
+#pragma unroll
+      for (int c = 1; c < C2; ++c) if (p[C1 + c] > bv) { bv = p[C1 + c]; b = c; }
+      d = t.veh_to_common[b];
+    } else if (d1 == t.cid_l1_human) {
+      int b = 0;
+      float bv = p[C1 + C2];
+#pragma unroll
+      for (int c = 1; c < C3; ++c) if (p[C1 + C2 + c] > bv) { bv = p[C1 + C2 + c]; b = c; }
+      d = t.hum_to_common[b];
+    } else {
+      d = t.l1_to_common[d1];
+    }
+    d = a.map[d];   // tf.gather(ocids2ncids, decs)
+    if (a.replace_voids) {
+      // top_k(l1_probabilities, 2) (stable: equal values keep the lower index first);
+      // l1_probabilities keep C1 channels (the segment-sum remap does not apply to them)
+      int d2 = -1;
+      float b2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < C1; ++c)
+        if (c != d1 && (d2 < 0 || p[c] > b2)) { b2 = p[c]; d2 = c; }
+      d = d == C1 - 1 ? d2 : d1;
+    }
+    a.out[id] = d;
+  }
+}
 }  // namespace
 
 int loss_head_blocks(int N, int Hl, int Wl) {
@@ -456,5 +541,19 @@ hipError_t launch_confusion(const int* labels, const int* decisions, long n, int
   if (g > 1024) g = 1024;
   hipLaunchKernelGGL(confusion_kernel, dim3((int)g), dim3(256), 0, s, labels, decisions, n,
                      num_classes, cm);
+  return hipGetLastError();
+}
+
+hipError_t launch_eval_decisions(const EvalArgs& a, const LossTables& t, hipStream_t s) {
+  const long total = (long)a.N * a.Ho * a.Wo;
+  if (total <= 0) return hipSuccess;
+  long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (t.c1 == 14 && t.c2 == 7 && t.c3 == 3)
+    hipLaunchKernelGGL((eval_decisions_kernel<14, 7, 3>), dim3((int)g), dim3(256), 0, s, a, t);
+  else if (t.c1 == 53 && t.c2 == 12 && t.c3 == 5)
+    hipLaunchKernelGGL((eval_decisions_kernel<53, 12, 5>), dim3((int)g), dim3(256), 0, s, a, t);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }

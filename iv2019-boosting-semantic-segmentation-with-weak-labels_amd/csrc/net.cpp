@@ -156,6 +156,7 @@ struct seg_ctx {
   // dy on the compute stream), so the dgrad -> BN-backward chain and the wgrads overlap
   // cross-replica BN (seg_set_bn_sync): per-layer moment exchange through the caller's hook
   seg_allreduce_fn sync_fn = nullptr;
+  int bn_infer = 0;   // seg_set_bn_inference: forward normalises with the moving statistics
   void* sync_user = nullptr;
   int sync_world = 1;
   float* sync_pack = nullptr;     // [2 * max C]
@@ -439,6 +440,12 @@ int conv_forward(Step& S, int li, const Act& x) {
   if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
   HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
+  if (c->bn_infer) {   // is_training=False: the moving statistics normalise (no exchange)
+    const long half = c->n_moving / 2;
+    HIPCALL(c, launch_bn_infer_finalize(c->moving + L.mv_off, c->moving + half + L.mv_off, L.co,
+                                        c->params + L.g_off, L.st, S.s));
+    return 0;
+  }
   const bool sync = c->sync_fn != nullptr;
   HIPCALL(c, launch_bn_stats_finalize(L.stats_part, M, L.co, conv_nt_stat_rows(S.dt, 0, a), c->stat_scratch,
                                       c->params + L.g_off, L.st, S.s, sync ? c->sync_pack : nullptr));
@@ -1293,6 +1300,35 @@ int seg_loss(seg_ctx* c, const int32_t* px, const float* bbox, const float* tag,
   HIPCALL(c, launch_loss_head(a, c->tables, s));
   HIPCALL(c, launch_loss_finalize(c->loss_part, c->loss_blocks, c->tables, c->ldl, c->loss_scale,
                                   c->loss_out, c->dzscale, s));
+  return 0;
+}
+
+int seg_set_bn_inference(seg_ctx* c, int on) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  c->bn_infer = on ? 1 : 0;
+  return 0;
+}
+
+int seg_predict(seg_ctx* c, const int32_t* cid_map, int n_map, int replace_voids, int out_h,
+                int out_w, int32_t* decisions_out, void* stream) {
+  NEED_BOUND(c);
+  const seg_cfg& g = c->cfg;
+  if (!cid_map || !decisions_out) return set_err(&c->err, -EINVAL, "null cid_map / decisions_out");
+  if (n_map != c->tables.n_pp)
+    return set_err(&c->err, -EINVAL, "cid map has %d entries, the model has %d training classes",
+                   n_map, c->tables.n_pp);
+  if (out_h < 1 || out_w < 1) return set_err(&c->err, -EINVAL, "bad output size %dx%d", out_h, out_w);
+  EvalArgs a{};
+  a.logits = (const float*)c->logits.p; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
+  a.ldl = c->ldl; a.H = g.height; a.W = g.width; a.Ho = out_h; a.Wo = out_w;
+  a.replace_voids = replace_voids ? 1 : 0; a.n_map = n_map; a.out = decisions_out;
+  int mx = -1;
+  for (int i = 0; i < n_map; ++i) mx = std::max(mx, (int)cid_map[i]);
+  for (int i = 0; i < n_map; ++i) {   // utils._replacevoids: -1 -> max + 1
+    if (cid_map[i] < -1) return set_err(&c->err, -EINVAL, "cid_map[%d] = %d", i, cid_map[i]);
+    a.map[i] = cid_map[i] == -1 ? mx + 1 : cid_map[i];
+  }
+  HIPCALL(c, launch_eval_decisions(a, c->tables, (hipStream_t)stream));
   return 0;
 }
 

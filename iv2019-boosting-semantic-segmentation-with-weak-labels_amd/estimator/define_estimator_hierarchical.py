@@ -22,7 +22,9 @@ from estimator.define_losses_hierarchical import define_losses
 from estimator.define_optimizer import DynamicLossScaler, define_optimizer
 from estimator.mode_keys import ModeKeys
 
-EstimatorSpec = namedtuple('EstimatorSpec', ['mode', 'predictions', 'loss', 'train_op', 'losses'])
+EstimatorSpec = namedtuple('EstimatorSpec',
+                           ['mode', 'predictions', 'loss', 'train_op', 'losses', 'eval_metric_ops'],
+                           defaults=(None,))
 
 
 class GlobalStep(object):
@@ -88,8 +90,10 @@ def define_estimator(mode, features, labels, model_fn, config, params):
     assert params.name_feature_extractor in {'resnet_v1_50', 'resnet_v1_101'}
     proimages = features['proimages']
     _, _, predictions = model_fn(mode, proimages, labels, config, params)
-    if mode != ModeKeys.TRAIN:
-        raise NotImplementedError('EVAL/PREDICT are out of scope of the native training path')
+    if mode == ModeKeys.EVAL:
+        return _eval_spec(predictions, labels, config, params)
+    if mode == ModeKeys.PREDICT:
+        return _predict_spec(predictions, features, params)
     global_step = get_or_create_global_step()
     ctx = predictions['_context']
     # fp16 storage: dynamic loss scaling (the scale must be set before the loss seeds the
@@ -111,3 +115,51 @@ def define_estimator(mode, features, labels, model_fn, config, params):
         return losses
 
     return EstimatorSpec(mode, predictions, losses['total'], train_op, losses)
+
+
+def _eval_spec(predictions, labels, config, params):
+    """EVAL branch (define_estimator_hierarchical.py:161-200): zero losses, decisions mapped
+    to evaluation cids, optionally void-replaced, nearest-neighbour resized to the label
+    size, and the streaming confusion matrix of this batch (labels rows, decisions columns),
+    max(tcids2ecids) + 1 classes. All of it runs on the device (seg_predict, seg_confusion)."""
+    import torch
+    from utils.utils import _replacevoids
+    if getattr(params, 'preserve_aspect_ratio', False):
+        raise NotImplementedError('evaluation with preserving aspect ratio is not implemented.')
+    losses = define_losses(ModeKeys.EVAL, predictions, labels, config, params)
+    ctx = predictions['_context']
+    prolabels = labels['prolabels']
+    tcids2ecids = list(params.training_cids2evaluation_cids)
+    decs = torch.empty(prolabels.shape, dtype=torch.int32, device=prolabels.device)
+    ctx.predict(tcids2ecids, decs, replace_voids=bool(getattr(params, 'replace_voids', False)))
+    nc = max(_replacevoids(tcids2ecids)) + 1
+    cm = torch.empty((nc, nc), dtype=torch.int32, device=prolabels.device)
+    ctx.confusion(prolabels.to(torch.int32).contiguous(), decs, nc, cm)
+    out = dict(predictions)
+    out['decisions'] = decs
+    return EstimatorSpec(ModeKeys.EVAL, out, losses['total'], None, losses,
+                         {'confusion_matrix': cm})
+
+
+def _predict_spec(predictions, features, params):
+    """PREDICT branch (define_estimator_hierarchical.py:202-232): decisions mapped to the
+    inference cids (optionally void-replaced) at network resolution; the low-resolution
+    logits stand in for the full-resolution probabilities (softmax of their align-corners
+    upsampling, which the fused head never materialises)."""
+    import torch
+    ctx = predictions['_context']
+    n = features['proimages'].shape[0]
+    decs = torch.empty((n, params.height_network if hasattr(params, 'height_network')
+                        else params.height_feature_extractor,
+                        params.width_network if hasattr(params, 'width_network')
+                        else params.width_feature_extractor),
+                       dtype=torch.int32, device=features['proimages'].device)
+    ctx.predict(list(params.training_cids2inference_cids), decs,
+                replace_voids=bool(getattr(params, 'replace_voids', False)))
+    out = {k: v for k, v in predictions.items()
+           if k in ('l1_logits', 'l2_vehicle_logits', 'l2_human_logits', '_context')}
+    out['decisions'] = decs
+    for k in ('rawimages', 'rawimagespaths'):
+        if k in features:
+            out[k] = features[k]
+    return EstimatorSpec(ModeKeys.PREDICT, out, None, None, None)

@@ -53,3 +53,34 @@ def batch(seed, nb_pp, nb_pb, nb_pi, h, w):
                 px=pixel_labels(rng, nb_pp, h, w),
                 bbox=bbox_labels(rng, nb_pb, h, w) if nb_pb else None,
                 tag=tag_labels(rng, nb_pi, h, w) if nb_pi else None)
+
+
+def evaluate_input(config, params, seed=1234, device=None):
+    """EVAL input_fn in the reference's contract (input_cityscapes.py evaluate_input):
+    endless seeded batches of ({'proimages'}, {'prolabels'}) as device tensors, Nb images
+    per rank at the network size, labels at (label_height, label_width) when the settings
+    carry them (default: the network size)."""
+    import torch
+    from input_pipelines.utils import get_temp_Nb
+    nb = get_temp_Nb(config, params.Nb)
+    h, w = params.height_feature_extractor, params.width_feature_extractor
+    hl = getattr(params, 'label_height', None) or h
+    wl = getattr(params, 'label_width', None) or w
+    dev = device or torch.device('cuda', torch.cuda.current_device())
+    rng = np.random.default_rng(seed)
+    while True:
+        imgs = torch.from_numpy(images(rng, nb, h, w)).to(dev)
+        labs = torch.from_numpy(pixel_labels(rng, nb, hl, wl).astype(np.int32)).to(dev)
+        yield {'proimages': imgs}, {'prolabels': labs}
+
+
+def predict_input(config, params, seed=4321, device=None):
+    """PREDICT input_fn: seeded ({'proimages'}, None) batches of Nb images."""
+    import torch
+    from input_pipelines.utils import get_temp_Nb
+    nb = get_temp_Nb(config, params.Nb)
+    h, w = params.height_feature_extractor, params.width_feature_extractor
+    dev = device or torch.device('cuda', torch.cuda.current_device())
+    rng = np.random.default_rng(seed)
+    while True:
+        yield {'proimages': torch.from_numpy(images(rng, nb, h, w)).to(dev)}, None

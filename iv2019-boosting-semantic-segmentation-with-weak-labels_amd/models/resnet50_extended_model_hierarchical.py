@@ -9,7 +9,10 @@ logits convs, and this function runs its forward pass on the device tensor ``fea
 
 ``predictions`` carries the LOW-RESOLUTION logits (the 8x align-corners upsampling of
 hierarchical.py:84-86 is fused into the loss head, which never materialises full-resolution
-logits); ``decisions`` is the full-resolution fused decision map filled by the loss head.
+logits); in TRAIN ``decisions`` is the full-resolution fused decision map filled by the loss
+head; in EVAL / PREDICT ``decisions`` is produced by ``seg_predict`` (no loss head) from the
+logits of a forward whose batch norm uses the moving statistics unless
+``batch_norm_accumulate_statistics`` is set (hierarchical.py:306-307).
 """
 from __future__ import annotations
 
@@ -38,18 +41,21 @@ def _validate_params(params):
         raise NotImplementedError('stride_feature_extractor must be 8')
 
 
-def sub_batches(config, params):
-    """Per-rank (per-tower) sub-batches: each of the three is split (get_temp_Nb)."""
+def sub_batches(config, params, mode=ModeKeys.TRAIN):
+    """Per-rank (per-tower) sub-batches: each of the three is split (get_temp_Nb).
+    EVAL / PREDICT batches are Nb per-pixel images (evaluate/predict input pipelines)."""
+    if mode != ModeKeys.TRAIN:
+        return (get_temp_Nb(config, params.Nb), 0, 0)
     return (get_temp_Nb(config, getattr(params, 'Nb_per_pixel', params.Nb)),
             get_temp_Nb(config, getattr(params, 'Nb_per_bbox', 0)),
             get_temp_Nb(config, getattr(params, 'Nb_per_image', 0)))
 
 
-def get_context(config, params, device=None):
+def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
     """The process's native context for these settings (created on first use)."""
     from seg_hip import SegContext
     import torch
-    nb_pp, nb_pb, nb_pi = sub_batches(config, params)
+    nb_pp, nb_pb, nb_pi = sub_batches(config, params, mode)
     depth = 101 if getattr(params, 'name_feature_extractor', 'resnet_v1_50') == 'resnet_v1_101' else 50
     pyramid = getattr(params, 'pyramid', None) or (
         'psp' if getattr(params, 'psp_module', False) else
@@ -81,11 +87,15 @@ def model(mode, features, labels, config, params):
     """Forward pass (hierarchical.py:17-141). ``features``: device tensor [N, hf, wf, 3]."""
     import torch
     _validate_params(params)
-    if mode != ModeKeys.TRAIN:
-        raise NotImplementedError('EVAL/PREDICT forward (moving-statistics BN) is out of scope '
-                                  'for the native training path (SURVEY §2 #15/#16)')
-    ctx = get_context(config, params)
+    ctx = get_context(config, params, mode=mode)
     assert features.shape[-1] == 3, 'features must be NHWC with 3 channels'
+    # tf.contrib.layers.batch_norm(is_training=batch_norm_accumulate_statistics)
+    # (hierarchical.py:40-49,306-307). TRAIN always accumulates statistics here (train.py
+    # sets the flag; a frozen-statistics backward is not built); EVAL / PREDICT follow it.
+    infer = mode != ModeKeys.TRAIN and not bool(
+        getattr(params, 'batch_norm_accumulate_statistics', False))
+    if getattr(ctx, 'bn_inference', False) != infer:
+        ctx.set_bn_inference(infer)
     ctx.forward(features.contiguous())
     _, _, logits = ctx.outputs()
     c1, c2, c3 = (53, 12, 5) if params.per_pixel_dataset_name == 'vistas' else (14, 7, 3)

@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = [
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
-    "seg_set_bn_sync",
+    "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict",
 ]
 
 # int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, hipStream_t stream)
@@ -100,6 +100,8 @@ def _load():
         "seg_found_inf": (ip, [vp, ctypes.POINTER(ctypes.c_void_p)]),
         "seg_set_bn_sync": (ip, [vp, SEG_ALLREDUCE_FN, vp, ip]),
         "seg_tag_labels": (ip, [vp, ip, ip, ip, vp, vp]),
+        "seg_set_bn_inference": (ip, [vp, ip]),
+        "seg_predict": (ip, [vp, ctypes.POINTER(ctypes.c_int32), ip, ip, ip, ip, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -220,6 +222,26 @@ class SegContext:
     def loss(self, px_labels=None, bbox_soft=None, tag_soft=None, decisions=None, stream=None):
         check(LIB.seg_loss(self.h, _ptr(px_labels), _ptr(bbox_soft), _ptr(tag_soft),
                            _ptr(decisions), _stream(stream)), self.h)
+
+    def set_bn_inference(self, on: bool):
+        """BN normalises with the moving statistics in later forwards (is_training=False,
+        the reference's default unless --batch_norm_accumulate_statistics)."""
+        check(LIB.seg_set_bn_inference(self.h, 1 if on else 0), self.h)
+        self.bn_inference = bool(on)
+
+    def predict(self, cid_map, out, replace_voids=False, stream=None):
+        """Decisions of the last forward mapped through ``cid_map`` (training -> eval/inference
+        cids, -1 = void), optionally void-replaced, nearest-neighbour resized to out's
+        [N, Ho, Wo] (device int32)."""
+        m = (ctypes.c_int32 * len(cid_map))(*[int(v) for v in cid_map])
+        import torch
+        n = self.cfg.nb_pp + self.cfg.nb_pb + self.cfg.nb_pi
+        if not (out.dtype == torch.int32 and out.dim() == 3 and out.is_contiguous()
+                and out.shape[0] == n and out.is_cuda):
+            raise ValueError(f"decisions buffer must be a contiguous device int32 [{n}, Ho, Wo]")
+        check(LIB.seg_predict(self.h, m, len(cid_map), 1 if replace_voids else 0,
+                              int(out.shape[1]), int(out.shape[2]), _ptr(out), _stream(stream)),
+              self.h)
 
     def backward(self, stream=None):
         check(LIB.seg_backward(self.h, _stream(stream)), self.h)

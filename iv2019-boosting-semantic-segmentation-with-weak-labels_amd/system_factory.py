@@ -173,12 +173,104 @@ class SemanticSegmentation(object):
                 ctx.momentum[p.offset:p.offset + p.numel].copy_(torch.as_tensor(mom[p.name]))
         step.value = int(state['global_step'])
 
-    def predict(self):
-        raise NotImplementedError('inference/visualisation is out of scope (SURVEY §2 #15)')
+    # ---- evaluation / prediction (system_factory.py:148-158,304-412) -------------------
+    def _cid_maps(self):
+        s = self._settings
+        tcids = list(range(s.output_Nclasses))
+        if s.lids_training_contain_unlabeled and not getattr(s, 'train_void_class', False):
+            tcids[-1] = -1   # ignore void if it was not trained
+        path = getattr(s, 'evaluation_problem_def_path', None)
+        if path:
+            with open(path, 'r') as fp:
+                s.evaluation_problem_def = json.load(fp)
+        else:
+            s.evaluation_problem_def = s.training_problem_def
+        s.training_cids2evaluation_cids = s.evaluation_problem_def.get(
+            'training_cids2evaluation_cids', list(tcids))
+        path = getattr(s, 'inference_problem_def_path', None)
+        if path:
+            with open(path, 'r') as fp:
+                s.inference_problem_def = json.load(fp)
+        else:
+            s.inference_problem_def = s.training_problem_def
+        s.training_cids2inference_cids = s.inference_problem_def.get(
+            'training_cids2inference_cids', list(tcids))
 
-    def evaluate(self):
-        raise NotImplementedError('evaluation is disabled in the reference (evaluate.py:82) '
-                                  'and out of scope here')
+    def _restore_for_eval(self, ctx, ckpt_path):
+        import torch
+        s = self._settings
+        if not ckpt_path:
+            ck = sorted(glob.glob(join(s.log_dir, 'model.ckpt-*.pt')),
+                        key=lambda p: int(re.findall(r'-(\d+)\.pt$', p)[0]))
+            ckpt_path = ck[-1] if ck else None
+        if not ckpt_path:
+            return 0
+        state = torch.load(ckpt_path, weights_only=True)
+        # restore_emas: evaluate the shadow (EMA) weights when asked and present
+        params = state.get('ema') if getattr(s, 'restore_emas', False) and 'ema' in state \
+            else state['params']
+        ctx.load_params(params)
+        if params is not state['params']:   # EMA excludes the moving statistics
+            ctx.load_params({k: v for k, v in state['params'].items() if 'moving_' in k})
+        return int(state['global_step'])
+
+    def evaluate(self, max_steps=None, log_fn=print):
+        """One pass over the eval input per checkpoint; returns [{'global_step', 'loss',
+        'confusion_matrix'}] with the void row/column dropped as the reference does."""
+        import numpy as np
+        import torch
+        from models.resnet50_extended_model_hierarchical import get_context
+        s = self._settings
+        self._cid_maps()
+        s.num_examples = int(s.Neval * s.height_network // s.height_feature_extractor *
+                             s.width_network // s.width_feature_extractor)
+        s.num_batches_per_epoch = int(s.num_examples / s.Nb)
+        s.num_eval_steps = s.num_batches_per_epoch if max_steps is None else \
+            min(max_steps, s.num_batches_per_epoch)
+        config = RunConfig(model_dir=s.log_dir)
+        labels_names = s.evaluation_problem_def['cids2labels']
+        void_exists = -1 in s.evaluation_problem_def['lids2cids']
+        if void_exists and not getattr(s, 'train_void_class', False):
+            labels_names = labels_names[:-1]
+        ckpts = [getattr(s, 'ckpt_path', None)]
+        if getattr(s, 'eval_all_ckpts', False):
+            ckpts = sorted(glob.glob(join(s.log_dir, 'model.ckpt-*.pt')),
+                           key=lambda p: int(re.findall(r'-(\d+)\.pt$', p)[0]))
+        ctx = get_context(config, s, mode=ModeKeys.EVAL)
+        all_metrics = []
+        for cp in ckpts:
+            gstep = self._restore_for_eval(ctx, cp)
+            cm = None
+            data = iter(self._input_fns['eval'](config, s))
+            for _ in range(s.num_eval_steps):
+                features, labels = next(data)
+                spec = self._estimator_fn(ModeKeys.EVAL, features, labels, config=config,
+                                          params=s)
+                c = spec.eval_metric_ops['confusion_matrix'].to(torch.int64)
+                cm = c if cm is None else cm + c
+            cm = cm.cpu().numpy().astype(np.int32)
+            if void_exists and not getattr(s, 'train_void_class', False):
+                cm = cm[:-1, :-1]
+            metrics = {'global_step': gstep, 'loss': 0.0, 'confusion_matrix': cm}
+            print_metrics_from_confusion_matrix(np.asarray(cm), labels_names,
+                                                printcmd=bool(log_fn))
+            all_metrics.append(metrics)
+        return all_metrics
+
+    def predict(self, max_steps=None):
+        """Generator of per-batch predictions dicts ('decisions' [N, H, W] device int32 in
+        inference cids, low-res logits, and the input's raw images/paths when given)."""
+        from models.resnet50_extended_model_hierarchical import get_context
+        s = self._settings
+        self._cid_maps()
+        config = RunConfig(model_dir=s.log_dir)
+        ctx = get_context(config, s, mode=ModeKeys.PREDICT)
+        self._restore_for_eval(ctx, getattr(s, 'ckpt_path', None))
+        for i, (features, _) in enumerate(self._input_fns['predict'](config, s)):
+            if max_steps is not None and i >= max_steps:
+                return
+            spec = self._estimator_fn(ModeKeys.PREDICT, features, None, config=config, params=s)
+            yield spec.predictions
 
 
 def _set_defaults(settings):

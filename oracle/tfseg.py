@@ -260,6 +260,17 @@ def resize_tables(n_in: int, n_out: int):
     return lo, hi, lerp
 
 
+def nearest_ac_index(n_in: int, n_out: int):
+    """TF 1.12 ResizeNearestNeighbor(align_corners=True) source rows: scale =
+    (in-1)/(out-1) in float32 (in/out when out == 1), in = min(roundf(o*scale), in-1)
+    (round half away from zero)."""
+    scale = (np.float32(n_in - 1) / np.float32(n_out - 1) if n_out > 1
+             else np.float32(n_in) / np.float32(n_out))
+    f = (np.arange(n_out, dtype=np.float32) * np.float32(scale)).astype(np.float32)
+    r = np.floor(f.astype(np.float64) + 0.5)   # f >= 0: roundf, exact in float64
+    return torch.as_tensor(np.minimum(r.astype(np.int64), n_in - 1))
+
+
 def resize_bilinear_ac(x, h_out: int, w_out: int):
     """align_corners bilinear with TF's arithmetic form:
     top = tl + (tr-tl)*xl; bottom = bl + (br-bl)*xl; out = top + (bottom-top)*yl."""
@@ -344,11 +355,22 @@ class OracleNet:
         self.p = {k: torch.tensor(v, dtype=dtype) for k, v in params.items()}
         self.batch_stats: Dict[str, tuple] = {}
         self.sync_bn = False   # cross-replica BN over a concatenated multi-replica batch
+        self.bn_inference = False   # EVAL / PREDICT with batch_norm_accumulate_statistics unset
 
     # -- building blocks -------------------------------------------------------------
     def conv_bn(self, x, name: str, relu: Optional[bool] = None, record: Dict = None):
         s = self.spec_by_name[name]
         y = conv_tf(x, self.p[f"{name}/weights"], s)
+        if self.bn_inference:   # is_training=False (hierarchical.py:306-307): moving statistics
+            mm = self.p[f"{name}/BatchNorm/moving_mean"]
+            mv = self.p[f"{name}/BatchNorm/moving_variance"]
+            sc = self.p[f"{name}/BatchNorm/gamma"] * torch.rsqrt(mv + BN_EPS)
+            out = (y - mm[None, :, None, None]) * sc[None, :, None, None] + \
+                self.p[f"{name}/BatchNorm/beta"][None, :, None, None]
+            if record is not None:
+                record[name] = y
+            act = s.relu if relu is None else relu
+            return torch.relu(out) if act else out
         out, m, v = bn_train(y, self.p[f"{name}/BatchNorm/gamma"], self.p[f"{name}/BatchNorm/beta"],
                              bessel=not self.sync_bn)
         self.batch_stats[name] = (m, v)
@@ -430,6 +452,29 @@ class OracleNet:
                             torch.where(l1d == t["cid_l1_human"], _t(t["hum_to_common"])[hd],
                                         _t(t["l1_to_common"])[l1d]))
         return up, probs, decs, fused
+
+    # -- EVAL / PREDICT decisions (define_estimator_hierarchical.py:161-194,215-232) ---
+    def eval_decisions(self, low, cid_map, out_h, out_w, replace_voids=False):
+        """_map_predictions_to_new_cids (:490-522) -> _replace_voids (:577-630) ->
+        _resize_predictions (:524-575) of the fused decisions; returns int64 [N, out_h, out_w].
+
+        The l1 probabilities keep their C1 channels: the segment-sum remap raises on a
+        len(cid_map) != C1 map and is skipped by the reference's bare except (:509-515), so
+        _replace_voids compares the MAPPED decisions with C1 - 1 and takes l1 top-k indices."""
+        _, probs, decs, fused = self.head_predictions(low)
+        m = np.asarray(cid_map, dtype=np.int64)
+        m = np.where(m == -1, m.max() + 1, m)                  # utils._replacevoids
+        assert len(m) != probs["l1_logits"].shape[1], "probability remap branch not restated"
+        d = torch.as_tensor(m)[fused]                          # tf.gather(ocids2ncids, decs)
+        if replace_voids:
+            p1 = probs["l1_logits"]                            # [N, C1, H, W]
+            c1 = p1.shape[1]
+            # top_k(k=2), stable: equal values keep the lower index first
+            order = torch.sort(-p1, dim=1, stable=True).indices
+            d = torch.where(d == c1 - 1, order[:, 1], order[:, 0])
+        hy = nearest_ac_index(self.cfg.height, out_h)
+        wx = nearest_ac_index(self.cfg.width, out_w)
+        return d[:, hy][:, :, wx]
 
     # -- losses (define_losses_hierarchical.py:98-210) ---------------------------------
     def losses(self, low, px_labels, bbox_soft=None, tag_soft=None):

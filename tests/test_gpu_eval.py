@@ -1,0 +1,204 @@
+"""EVAL / PREDICT path through the C ABI against the oracle.
+
+* moving-statistics batch norm (is_training = batch_norm_accumulate_statistics = False,
+  models/resnet50_extended_model_hierarchical.py:40-49,306-307): low-res logits of an
+  inference-mode forward vs the oracle's, 1e-3 relative (or 4x the fp32 oracle's own gap);
+  the moving statistics are the oracle's batch statistics of another batch, so activations
+  stay in the range real checkpoints give;
+* seg_predict (define_estimator_hierarchical.py:161-232): decisions mapped to evaluation cids,
+  optionally void-replaced, nearest-neighbour resized to the label size. The oracle is fed the
+  NATIVE low-res logits so the decision logic is checked by itself: equal up to fp32 near-ties
+  of the softmax argmax (at most 0.1 % of the pixels; 0 expected);
+* the streaming confusion matrix of the EVAL spec, and SemanticSegmentation.evaluate /
+  .predict end to end on synthetic input.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.tfseg import OracleNet, SegConfig, confusion_matrix, init_params
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROBLEM = os.path.join(REPO, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
+                       "problem_definitions", "cityscapes", "problem01.json")
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _params_with_moving_stats(cfg, seed=3):
+    """init_params + moving statistics = the oracle's batch statistics of another batch."""
+    from input_pipelines.synthetic import batch
+    params = init_params(cfg, seed=seed)
+    other = batch(99, cfg.nb, 0, 0, cfg.height, cfg.width)
+    net = OracleNet(cfg, params, dtype=torch.float64)
+    net.forward(torch.as_tensor(other["images"]))
+    for name, (m, v) in net.batch_stats.items():
+        params[f"{name}/BatchNorm/moving_mean"] = m.numpy()
+        params[f"{name}/BatchNorm/moving_variance"] = v.numpy()
+    # non-trivial affine parameters too
+    rng = np.random.default_rng(5)
+    for k in params:
+        if k.endswith("/gamma"):
+            params[k] = 1.0 + 0.1 * rng.standard_normal(params[k].shape)
+        elif k.endswith("/beta"):
+            params[k] = 0.1 * rng.standard_normal(params[k].shape)
+    return {k: np.asarray(v, np.float32) for k, v in params.items()}
+
+
+def _ctx(cfg, dtype="fp32"):
+    from seg_hip import SegContext
+    return SegContext(depth=cfg.depth, pyramid=cfg.pyramid, height=cfg.height, width=cfg.width,
+                      nb_pp=cfg.nb_pp, nb_pb=cfg.nb_pb, nb_pi=cfg.nb_pi, dtype=dtype)
+
+
+CFGS = [SegConfig(height=64, width=128, nb_pp=2, pyramid="psp"),
+        SegConfig(height=48, width=64, nb_pp=1, pyramid="aspp")]
+
+
+@pytest.mark.parametrize("cfg", CFGS, ids=lambda c: f"{c.height}x{c.width}-{c.pyramid}")
+def test_inference_bn_forward_fp32(cuda, cfg):
+    from input_pipelines.synthetic import batch
+    params = _params_with_moving_stats(cfg)
+    data = batch(11, cfg.nb, 0, 0, cfg.height, cfg.width)
+    ctx = _ctx(cfg)
+    ctx.load_params(params)
+    ctx.set_bn_inference(True)
+    ctx.forward(torch.as_tensor(data["images"]).to(cuda))
+    _, _, lg = ctx.outputs()
+    lg = lg.cpu().numpy().copy()
+    outs = {}
+    for dt in (torch.float64, torch.float32):
+        net = OracleNet(cfg, params, dtype=dt)
+        net.bn_inference = True
+        outs[dt] = {k: v.detach() for k, v in net.forward(torch.as_tensor(data["images"])).items()}
+    c1, c2, c3 = 14, 7, 3
+    for key, a, b in (("l1_logits", 0, c1), ("l2_vehicle_logits", c1, c1 + c2),
+                      ("l2_human_logits", c1 + c2, c1 + c2 + c3)):
+        ref = outs[torch.float64][key].permute(0, 2, 3, 1).numpy()
+        gap = _rel(outs[torch.float32][key].permute(0, 2, 3, 1).numpy(), ref)
+        assert _rel(lg[..., a:b], ref) < max(1e-3, 4 * gap), (key, gap)
+    # the training-mode forward of the same context differs (batch statistics)
+    ctx.set_bn_inference(False)
+    ctx.forward(torch.as_tensor(data["images"]).to(cuda))
+    _, _, lg_train = ctx.outputs()
+    assert _rel(lg_train.cpu().numpy()[..., :c1], lg[..., :c1]) > 1e-2
+    ctx.close()
+
+
+MAPS = {
+    "identity": list(range(19)) + [-1],
+    # merge some classes, ignore others (-1 -> void = max + 1)
+    "merge": [0, 0, 1, 1, 2, -1, 3, 3, 4, 5, 6, 7, 7, 8, 8, 8, 9, 9, 9, -1],
+}
+
+
+@pytest.mark.parametrize("replace_voids", [False, True])
+@pytest.mark.parametrize("out_hw", [(64, 128), (32, 64), (128, 256), (45, 77)])
+@pytest.mark.parametrize("mapname", sorted(MAPS))
+def test_predict_decisions(cuda, mapname, out_hw, replace_voids):
+    from input_pipelines.synthetic import batch
+    cfg = CFGS[0]
+    params = _params_with_moving_stats(cfg)
+    data = batch(12, cfg.nb, 0, 0, cfg.height, cfg.width)
+    ctx = _ctx(cfg)
+    ctx.load_params(params)
+    ctx.set_bn_inference(True)
+    ctx.forward(torch.as_tensor(data["images"]).to(cuda))
+    _, _, lg = ctx.outputs()
+    out = torch.full((cfg.nb,) + out_hw, -7, dtype=torch.int32, device=cuda)
+    ctx.predict(MAPS[mapname], out, replace_voids=replace_voids)
+    nat = out.cpu().numpy()
+    low = lg.cpu().permute(0, 3, 1, 2).contiguous()
+    c1, c2 = 14, 7
+    net = OracleNet(cfg, params, dtype=torch.float32)
+    lowd = {"l1_logits": low[:, :c1], "l2_vehicle_logits": low[:, c1:c1 + c2],
+            "l2_human_logits": low[:, c1 + c2:c1 + c2 + 3]}
+    ref = net.eval_decisions(lowd, MAPS[mapname], out_hw[0], out_hw[1],
+                             replace_voids=replace_voids).numpy()
+    assert nat.shape == ref.shape and (nat >= 0).all()
+    mism = float(np.mean(nat != ref))
+    assert mism <= 1e-3, mism
+    ctx.close()
+
+
+def test_predict_rejects_bad_map(cuda):
+    cfg = CFGS[0]
+    ctx = _ctx(cfg)
+    out = torch.zeros((cfg.nb, 8, 8), dtype=torch.int32, device=cuda)
+    with pytest.raises(RuntimeError):
+        ctx.predict(list(range(10)), out)
+    with pytest.raises(ValueError):
+        ctx.predict(MAPS["identity"], torch.zeros((cfg.nb + 1, 8, 8), dtype=torch.int32,
+                                                  device=cuda))
+    ctx.close()
+
+
+def _eval_settings(tmp_path, nb=2, h=64, w=128, neval=4):
+    from models.resnet50_extended_model_hierarchical import add_model_arguments
+    from utils.utils import SemanticSegmentationArguments
+    from estimator.mode_keys import ModeKeys
+    a = SemanticSegmentationArguments(mode=ModeKeys.EVAL)
+    add_model_arguments(a.argparser)
+    s = a.parse_args([str(tmp_path), str(neval), PROBLEM, "--Nb", str(nb), "--psp_module",
+                      "--height_feature_extractor", str(h), "--width_feature_extractor", str(w),
+                      "--compute_dtype", "fp32"])
+    s.per_pixel_dataset_name = "cityscapes"
+    return s
+
+
+def test_evaluate_end_to_end(cuda, tmp_path):
+    """SemanticSegmentation.evaluate(): per-batch EVAL specs, device confusion matrices summed
+    over the pass, void row/column dropped (system_factory.py:395-405)."""
+    from input_pipelines.synthetic import evaluate_input
+    from models.resnet50_extended_model_hierarchical import model
+    from system_factory import SemanticSegmentation
+    s = _eval_settings(tmp_path)
+    system = SemanticSegmentation({"eval": evaluate_input}, model, s)
+    res = system.evaluate()
+    assert len(res) == 1
+    cm = res[0]["confusion_matrix"]
+    assert cm.shape == (19, 19) and cm.dtype == np.int32
+    # the same batches through the oracle-side confusion of the native decisions
+    st = system.settings
+    from estimator.define_estimator_hierarchical import define_estimator
+    from system_factory import RunConfig
+    from estimator.mode_keys import ModeKeys
+    total = np.zeros((20, 20), np.int64)
+    data = evaluate_input(RunConfig(), st)
+    for _ in range(st.num_eval_steps):
+        f, l = next(data)
+        spec = define_estimator(ModeKeys.EVAL, f, l, model, RunConfig(), st)
+        total += confusion_matrix(l["prolabels"].cpu().numpy(),
+                                  spec.predictions["decisions"].cpu().numpy(), 20)
+        assert float(spec.loss) == 0.0
+    np.testing.assert_array_equal(cm, total[:-1, :-1])
+    assert st.num_eval_steps == 2
+
+
+def test_predict_end_to_end(cuda, tmp_path):
+    from input_pipelines.synthetic import predict_input
+    from models.resnet50_extended_model_hierarchical import model
+    from system_factory import SemanticSegmentation
+    from utils.utils import SemanticSegmentationArguments
+    from estimator.mode_keys import ModeKeys
+    from models.resnet50_extended_model_hierarchical import add_model_arguments
+    a = SemanticSegmentationArguments(mode=ModeKeys.PREDICT)
+    add_model_arguments(a.argparser)
+    s = a.parse_args([str(tmp_path), PROBLEM, str(tmp_path / "pred"), "--Nb", "1",
+                      "--height_feature_extractor", "48", "--width_feature_extractor", "64",
+                      "--compute_dtype", "fp32"])
+    s.per_pixel_dataset_name = "cityscapes"
+    system = SemanticSegmentation({"predict": predict_input}, model, s)
+    preds = list(system.predict(max_steps=2))
+    assert len(preds) == 2
+    for p in preds:
+        d = p["decisions"].cpu().numpy()
+        assert d.shape == (1, 48, 64) and d.min() >= 0 and d.max() <= 19

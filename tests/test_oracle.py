@@ -185,3 +185,45 @@ def test_oracle_cross_replica_bn_duplicate_replicas():
         torch.testing.assert_close(stats2[name][0], m, rtol=1e-9, atol=1e-10)
         # biased global variance over 2n samples vs the Bessel-corrected one over n
         assert torch.all(stats2[name][1] <= v + 1e-12)
+
+
+def test_nearest_align_corners_known_answers():
+    """TF 1.12 ResizeNearestNeighbor(align_corners=True): in = min(roundf(o*(in-1)/(out-1)),
+    in-1), half away from zero (used by _resize_predictions,
+    define_estimator_hierarchical.py:566-570)."""
+    from oracle.tfseg import nearest_ac_index
+    assert nearest_ac_index(4, 4).tolist() == [0, 1, 2, 3]
+    assert nearest_ac_index(5, 3).tolist() == [0, 2, 4]
+    assert nearest_ac_index(3, 5).tolist() == [0, 1, 1, 2, 2]     # 0.5 -> 1, 1.5 -> 2
+    assert nearest_ac_index(2, 4).tolist() == [0, 0, 1, 1]        # 1/3, 2/3
+    assert nearest_ac_index(7, 1).tolist() == [0]
+
+
+def test_oracle_eval_decisions_map_replace_resize():
+    """eval_decisions on hand-built logits: the fused decision, the cid map (with -1 -> void),
+    the _replace_voids rule (mapped decision == C1 - 1 -> l1 top-2 index, else l1 top-1) and
+    the nearest-neighbour resize."""
+    import torch
+    from oracle.tfseg import OracleNet, SegConfig, init_params
+    cfg = SegConfig(height=16, width=16, nb_pp=1, pyramid="none")
+    net = OracleNet(cfg, init_params(cfg, seed=0))
+    low = {"l1_logits": torch.zeros(1, 14, 2, 2), "l2_vehicle_logits": torch.zeros(1, 7, 2, 2),
+           "l2_human_logits": torch.zeros(1, 3, 2, 2)}
+    low["l1_logits"][:, 5] = 4.0           # l1 class 5 -> cid 5 everywhere
+    low["l1_logits"][:, 2] = 3.0           # runner-up: 2
+    ident = list(range(19)) + [-1]
+    d = net.eval_decisions(low, ident, 16, 16)
+    assert d.shape == (1, 16, 16) and (d == 5).all()
+    m = list(ident)
+    m[5] = -1                              # ignored -> void = 19
+    assert (net.eval_decisions(low, m, 8, 8) == 19).all()
+    m2 = list(ident)
+    m2[5] = 13                             # mapped decision == C1 - 1 -> top-2 index
+    assert (net.eval_decisions(low, m2, 4, 4, replace_voids=True) == 2).all()
+    assert (net.eval_decisions(low, ident, 4, 4, replace_voids=True) == 5).all()
+    # vehicle branch: l1 argmax 12 (vehicle) -> l2 vehicle decision through veh_to_common
+    low["l1_logits"][:, 12] = 9.0
+    low["l2_vehicle_logits"][:, 3] = 1.0
+    d = net.eval_decisions(low, ident, 3, 3)
+    from oracle.tfseg import CITYSCAPES
+    assert (d == CITYSCAPES["veh_to_common"][3]).all()
