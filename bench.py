@@ -79,6 +79,7 @@ def main():
                     help="BASELINE.json workload preset (per-GPU share); C2 is the metric's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-eval", action="store_true")
     args = ap.parse_args()
 
     import numpy as np
@@ -239,6 +240,34 @@ def main():
         ctx.loss(px, bbox, tag, dec)
         cm = confusion_matrix(ctx, px, dec[:nb_pp], 20)
         miou = round(float(mean_iou_from_cm(cm)), 5)
+    # EVAL path (define_estimator_hierarchical.py:161-194) on the same resident batch, outside
+    # the timed training region: moving-statistics BN forward + seg_predict (fused decisions,
+    # cid map, nearest resize at label size = network size) + device confusion matrix
+    ev = None
+    if not args.no_eval and nb_pp:
+        from estimator.define_metrics import confusion_matrix
+        from utils.utils import metrics_from_confusion_matrix
+        cmap = list(range(19)) + [-1]
+        edec = torch.empty((nb_pp + nb_pb + nb_pi, H, W), dtype=torch.int32, device=dev)
+        ctx.set_bn_inference(True)
+
+        def eval_batch():
+            ctx.forward(img)
+            ctx.predict(cmap, edec)
+            return confusion_matrix(ctx, px, edec[:nb_pp], 20)
+        eval_batch()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            ecm = eval_batch()
+        torch.cuda.synchronize()
+        te = (time.perf_counter() - t0) / 3
+        ctx.set_bn_inference(False)
+        _, _, emiou, _, _ = metrics_from_confusion_matrix(
+            np.asarray(ecm.cpu().numpy() if hasattr(ecm, "cpu") else ecm, np.int32)[:-1, :-1])
+        ev = {"images_per_sec_per_gpu": round(NB / te, 3), "ms_per_batch": round(te * 1e3, 2),
+              "batch": NB, "miou_eval": round(float(emiou), 3),
+              "what": "moving-statistics BN forward + seg_predict + confusion (3 batches)"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C2":
         cpu = cpu_baseline(threads=min(16, os.cpu_count() or 1), pyramid=args.pyramid)
@@ -258,6 +287,7 @@ def main():
                           "image": [H, W], "parallelism": f"dp{world}"},
                "losses_last_step": [round(float(x), 5) for x in lv[:4]],
                "miou_train_summary": miou,
+               "eval": ev,
                "loss_scale": None if scaler is None else {
                    "scale": scaler.scale, "skipped_warmup": skipped0, "calibration_steps": calib,
                    "skipped_timed": scaler.skipped - skipped0},

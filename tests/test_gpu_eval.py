@@ -202,3 +202,23 @@ def test_predict_end_to_end(cuda, tmp_path):
     for p in preds:
         d = p["decisions"].cpu().numpy()
         assert d.shape == (1, 48, 64) and d.min() >= 0 and d.max() <= 19
+
+
+def test_evaluate_script_main(cuda, tmp_path):
+    """evaluate.py main: the reference's command line, metrics written to <log_dir>/eval."""
+    import importlib.util
+    path = os.path.join(REPO, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
+                        "evaluate.py")
+    spec = importlib.util.spec_from_file_location("seg_evaluate_main", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    res = mod.main([str(tmp_path), "2", PROBLEM, "cityscapes", "--Nb", "1",
+                    "--height_feature_extractor", "48", "--width_feature_extractor", "64",
+                    "--compute_dtype", "fp32"])
+    # Neval 2 at Nb 1: two batches; the void row / column are dropped from the counts
+    assert len(res) == 1 and 0 < int(res[0]["confusion_matrix"].sum()) <= 2 * 48 * 64
+    txt = open(tmp_path / "eval" / "all_metrics.txt").read()
+    assert txt.startswith("00000 ") and len(txt.split()) > 3   # step, global acc, mean acc, mIoU, ...
+    z = np.load(tmp_path / "eval" / "all_metrics.npz")
+    assert z["confusion_matrix"].shape == (1, 19, 19)
+
