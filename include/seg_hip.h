@@ -30,6 +30,7 @@
  */
 #ifndef SEG_HIP_H
 #define SEG_HIP_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -114,6 +115,11 @@ int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions,
 int seg_set_bn_inference(seg_ctx* ctx, int on);
 int seg_predict(seg_ctx* ctx, const int32_t* cid_map, int n_map, int replace_voids, int out_h,
                 int out_w, int32_t* decisions_out, void* stream);
+
+/* checkpoint interop (define_initializers.py:72-131, define_savers.py:38-66): CRC-32C of
+ * host bytes, continuing from `crc` (0 to start) — the checksum TF tensor bundles
+ * (<prefix>.index / <prefix>.data-*) keep per tensor and per table block. Host-only. */
+uint32_t seg_crc32c(uint32_t crc, const void* data, size_t n);
 
 /* loss scaling (fp16 storage, BASELINE config C5: fp16 with fp32 master gradients). The
  * gradient seed of seg_loss is multiplied by `scale`; seg_apply_update first flags non-finite

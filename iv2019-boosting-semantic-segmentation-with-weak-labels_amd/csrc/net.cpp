@@ -1646,3 +1646,43 @@ int seg_op_conv_wgrad_cfg(int dtype, const void* dy, int N, int Ho, int Wo, int 
 }
 
 }  // extern "C"
+
+// ---- checkpoint interop: CRC-32C (Castagnoli) of host bytes, the checksum TF 1.12 tensor
+// bundles store per tensor and per table block (tensorflow/core/lib/hash/crc32c.h), used by
+// utils/tf_checkpoint.py to read / write <prefix>.index + <prefix>.data-* checkpoints
+namespace {
+struct Crc32cTables {
+  uint32_t t[8][256];
+  Crc32cTables() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+  }
+};
+const Crc32cTables& crc_tables() {
+  static const Crc32cTables tb;
+  return tb;
+}
+}  // namespace
+
+extern "C" uint32_t seg_crc32c(uint32_t crc, const void* data, size_t n) {
+  const uint32_t(*t)[256] = crc_tables().t;
+  const uint8_t* p = (const uint8_t*)data;
+  uint32_t c = ~crc;
+  while (n >= 8) {   // slicing-by-8
+    uint32_t lo, hi;
+    memcpy(&lo, p, 4);
+    memcpy(&hi, p + 4, 4);
+    lo ^= c;
+    c = t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^
+        t[3][hi & 0xFF] ^ t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) c = t[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
+  return ~c;
+}

@@ -158,12 +158,27 @@ class SemanticSegmentation(object):
         if ctx.ema is not None:
             state['ema'] = ctx.named('ema')
         torch.save(state, join(self._settings.log_dir, f'model.ckpt-{global_step}.pt'))
+        if getattr(self._settings, 'tf_checkpoints', False):
+            # the reference's Saver layout: <log_dir>/model.ckpt-<step>.{index,data-*}
+            from utils.tf_checkpoint import export_checkpoint
+            export_checkpoint(ctx, join(self._settings.log_dir, f'model.ckpt-{global_step}'),
+                              global_step)
 
     def _maybe_restore(self, ctx, step):
         import torch
         ck = sorted(glob.glob(join(self._settings.log_dir, 'model.ckpt-*.pt')),
                     key=lambda p: int(re.findall(r'-(\d+)\.pt$', p)[0]))
         if not ck:
+            tf_ck = sorted(glob.glob(join(self._settings.log_dir, 'model.ckpt-*.index')),
+                           key=lambda p: int(re.findall(r'-(\d+)\.index$', p)[0]))
+            if tf_ck:   # continue from a TF-format checkpoint in log_dir
+                from utils.tf_checkpoint import import_checkpoint
+                step.value = import_checkpoint(ctx, tf_ck[-1][:-len('.index')])
+            elif getattr(self._settings, 'init_ckpt_path', ''):
+                # define_initializers.replace_initializers: warm start (e.g. ImageNet)
+                from utils.tf_checkpoint import warm_start
+                warm_start(ctx, self._settings.init_ckpt_path,
+                           psp_module=bool(getattr(self._settings, 'psp_module', False)))
             return
         state = torch.load(ck[-1], weights_only=True)
         ctx.load_params(state['params'])

@@ -77,6 +77,8 @@ class SemanticSegmentationArguments(object):
         p.add_argument('--momentum', type=float, default=0.9)
         p.add_argument('--use_nesterov', action='store_true')
         p.add_argument('--distribute', action='store_true')
+        # build-side: also write the reference's TF V2 checkpoints (utils/tf_checkpoint.py)
+        p.add_argument('--tf_checkpoints', action='store_true')
 
     # utils/utils.py:121-146
     def add_inference_arguments(self):

@@ -1,0 +1,68 @@
+"""Checkpoint interop through a native context: a TF-format export
+(model variables under their TF names in HWIO, Momentum slots, global_step) restores a
+fresh context bit-exactly; an ImageNet-style warm start (define_initializers.py:72-131)
+initialises exactly the encoder from a slim-named checkpoint; the training facade continues
+from TF-format checkpoints in log_dir."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(**kw):
+    from seg_hip import SegContext
+    a = dict(depth=50, pyramid="psp", height=64, width=128, nb_pp=1, dtype="fp32")
+    a.update(kw)
+    return SegContext(**a)
+
+
+def test_export_import_round_trip(cuda, tmp_path):
+    from models.initializers import init_params
+    from utils.tf_checkpoint import export_checkpoint, import_checkpoint, list_variables
+    a = _ctx()
+    a.load_params(init_params(a.param_info, seed=7))
+    a.moving.uniform_(0.5, 1.5)
+    a.momentum.normal_()
+    pre = str(tmp_path / "model.ckpt-42")
+    export_checkpoint(a, pre, 42)
+    names = dict(list_variables(pre))
+    w = [p for p in a.param_info if p.kind == "weights"][0]
+    assert names[w.name] == [w.shape[1], w.shape[2], w.shape[3], w.shape[0]]   # HWIO
+    assert w.name + "/Momentum" in names and "global_step" in names
+    b = _ctx()
+    assert import_checkpoint(b, pre) == 42
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params) and torch.equal(a.moving, b.moving)
+    assert torch.equal(a.momentum, b.momentum)
+    a.close()
+    b.close()
+
+
+def test_warm_start_from_slim_names(cuda, tmp_path):
+    from models.initializers import init_params
+    from utils.tf_checkpoint import save_checkpoint, tf_shapes, warm_start
+    ctx = _ctx()
+    ctx.load_params(init_params(ctx.param_info, seed=1))
+    before = ctx.named("params")
+    shapes = tf_shapes(ctx)
+    rng = np.random.default_rng(3)
+    pre = "feature_extractor/base/"
+    ck = {n[len(pre):]: rng.standard_normal(s).astype(np.float32)
+          for n, s in shapes.items() if n.startswith(pre)}
+    ck["resnet_v1_50/logits/weights"] = np.zeros((1, 1, 2048, 1000), np.float32)
+    ck["global_step"] = np.array(0, np.int64)
+    save_checkpoint(str(tmp_path / "resnet_v1_50.ckpt"), ck)
+    mapping = warm_start(ctx, str(tmp_path / "resnet_v1_50.ckpt"), psp_module=True)
+    after = ctx.named("params")
+    enc = {n for n in shapes if n.startswith(pre)}
+    assert set(mapping.values()) == enc
+    for p in ctx.param_info:
+        if p.name in enc:
+            v = ck[p.name[len(pre):]]
+            if p.kind == "weights":
+                v = v.transpose(3, 0, 1, 2)
+            np.testing.assert_array_equal(after[p.name].reshape(-1), v.reshape(-1))
+        else:
+            np.testing.assert_array_equal(after[p.name], before[p.name])
+    ctx.close()

@@ -14,7 +14,7 @@ HEADER = os.path.join(REPO, "include", "seg_hip.h")
 
 def _declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(seg_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(seg_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol():
