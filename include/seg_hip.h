@@ -116,6 +116,17 @@ int seg_set_bn_inference(seg_ctx* ctx, int on);
 int seg_predict(seg_ctx* ctx, const int32_t* cid_map, int n_map, int replace_voids, int out_h,
                 int out_w, int32_t* decisions_out, void* stream);
 
+/* input preprocessing (input_cityscapes.py:66-96,190-209), after the host
+ * decodes TFRecord -> tf.train.Example -> PNG (input_pipelines/tfrecords.py):
+ * seg_prepare_images: raw uint8 [n][src_h][src_w][3] -> convert_image_dtype -> bilinear
+ *   resize_images (align_corners = False) to H x W -> from_0_1_to_m1_1 -> fp32 [n][H][W][3]
+ * seg_prepare_labels: raw uint8 label ids [n][src_h][src_w] -> lids2cids[n_lids] (-1 = void
+ *   -> max + 1) -> nearest resize to H x W -> int32 [n][H][W] (-1 for ids outside the table) */
+int seg_prepare_images(const uint8_t* raw, int n, int src_h, int src_w, int H, int W, float* out,
+                       void* stream);
+int seg_prepare_labels(const uint8_t* raw, int n, int src_h, int src_w, int H, int W,
+                       const int32_t* lids2cids, int n_lids, int32_t* out, void* stream);
+
 /* checkpoint interop (define_initializers.py:72-131, define_savers.py:38-66): CRC-32C of
  * host bytes, continuing from `crc` (0 to start) — the checksum TF tensor bundles
  * (<prefix>.index / <prefix>.data-*) keep per tensor and per table block. Host-only. */

@@ -14,6 +14,7 @@
 
 #include "../../include/seg_hip.h"
 #include "bn.h"
+#include "input.h"
 #include "conv.h"
 #include "loss.h"
 #include "labels.h"
@@ -1464,6 +1465,29 @@ int seg_tag_labels(const float* tags, int n, int H, int W, float* out, void* str
     return set_err(nullptr, -EINVAL, "seg_tag_labels: bad arguments");
   hipError_t e = launch_tag_labels(tags, n, H, W, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_tag_labels");
+}
+
+int seg_prepare_images(const uint8_t* raw, int n, int src_h, int src_w, int H, int W, float* out,
+                       void* stream) {
+  if (n < 0 || src_h <= 0 || src_w <= 0 || H <= 0 || W <= 0 || (n > 0 && (!raw || !out)))
+    return set_err(nullptr, -EINVAL, "seg_prepare_images: bad arguments");
+  hipError_t e = launch_prepare_images(raw, n, src_h, src_w, H, W, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_prepare_images");
+}
+
+int seg_prepare_labels(const uint8_t* raw, int n, int src_h, int src_w, int H, int W,
+                       const int32_t* lids2cids, int n_lids, int32_t* out, void* stream) {
+  if (n < 0 || src_h <= 0 || src_w <= 0 || H <= 0 || W <= 0 || (n > 0 && (!raw || !out)) ||
+      !lids2cids || n_lids <= 0 || n_lids > SEG_MAX_LIDS)
+    return set_err(nullptr, -EINVAL, "seg_prepare_labels: bad arguments");
+  LidMap m{};
+  m.n = n_lids;
+  int mx = -1;
+  for (int i = 0; i < n_lids; ++i) mx = std::max(mx, (int)lids2cids[i]);
+  for (int i = 0; i < n_lids; ++i)   // utils._replacevoids: -1 -> max + 1
+    m.cid[i] = lids2cids[i] == -1 ? mx + 1 : lids2cids[i];
+  hipError_t e = launch_prepare_labels(raw, n, src_h, src_w, H, W, m, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_prepare_labels");
 }
 
 int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* ld, int* dtype) {

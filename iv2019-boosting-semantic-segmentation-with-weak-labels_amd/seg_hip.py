@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = [
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
     "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict",
-    "seg_crc32c",
+    "seg_crc32c", "seg_prepare_images", "seg_prepare_labels",
 ]
 
 # int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, hipStream_t stream)
@@ -102,6 +102,9 @@ def _load():
         "seg_set_bn_sync": (ip, [vp, SEG_ALLREDUCE_FN, vp, ip]),
         "seg_tag_labels": (ip, [vp, ip, ip, ip, vp, vp]),
         "seg_set_bn_inference": (ip, [vp, ip]),
+        "seg_prepare_images": (ip, [vp, ip, ip, ip, ip, ip, vp, vp]),
+        "seg_prepare_labels": (ip, [vp, ip, ip, ip, ip, ip, ctypes.POINTER(ctypes.c_int32), ip,
+                                    vp, vp]),
         "seg_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, vp, ctypes.c_size_t]),
         "seg_predict": (ip, [vp, ctypes.POINTER(ctypes.c_int32), ip, ip, ip, ip, vp, vp]),
     }

@@ -271,6 +271,48 @@ def nearest_ac_index(n_in: int, n_out: int):
     return torch.as_tensor(np.minimum(r.astype(np.int64), n_in - 1))
 
 
+def prepare_images_np(raw_u8, H: int, W: int):
+    """Eval/train image preprocessing (input_cityscapes.py:190-209, 66-96):
+    tf.image.convert_image_dtype (uint8 -> x * float32(1/255)), ResizeBilinear with
+    align_corners=False (TF 1.12 legacy scaler: scale = in/out, in_f = o*scale, lo = (int),
+    hi = min(lo+1, in-1), lerp = in_f - lo, all float32), from_0_1_to_m1_1 ((x-0.5)/0.5).
+    raw_u8 [n, h, w, 3] -> float32 [n, H, W, 3]."""
+    raw = np.asarray(raw_u8)
+    x = raw.astype(np.float32) * np.float32(1.0 / 255.0)
+
+    def tables(n_in, n_out):
+        scale = np.float32(np.float32(n_in) / np.float32(n_out))
+        fin = (np.arange(n_out, dtype=np.float32) * scale).astype(np.float32)
+        lo = fin.astype(np.int64)
+        hi = np.minimum(lo + 1, n_in - 1)
+        return lo, hi, (fin - lo.astype(np.float32)).astype(np.float32)
+    yl, yh, ylr = tables(raw.shape[1], H)
+    xl, xh, xlr = tables(raw.shape[2], W)
+    xlr = xlr[None, None, :, None]
+    ylr = ylr[None, :, None, None]
+    tl, tr = x[:, yl][:, :, xl], x[:, yl][:, :, xh]
+    bl, br = x[:, yh][:, :, xl], x[:, yh][:, :, xh]
+    top = tl + (tr - tl) * xlr
+    bot = bl + (br - bl) * xlr
+    v = (top + (bot - top) * ylr).astype(np.float32)
+    return ((v - np.float32(0.5)) / np.float32(0.5)).astype(np.float32)
+
+
+def prepare_labels_np(raw_u8, H: int, W: int, lids2cids):
+    """tf.gather(_replacevoids(lids2cids), label) then ResizeNearestNeighbor (align_corners
+    False: src = min(floorf(o * float32(in/out)), in-1)). [n, h, w] uint8 -> int32."""
+    raw = np.asarray(raw_u8)
+    m = np.asarray(lids2cids, np.int64)
+    m = np.where(m == -1, m.max() + 1, m)
+
+    def src(n_in, n_out):
+        scale = np.float32(np.float32(n_in) / np.float32(n_out))
+        f = (np.arange(n_out, dtype=np.float32) * scale).astype(np.float32)
+        return np.minimum(np.floor(f).astype(np.int64), n_in - 1)
+    lab = m[raw.astype(np.int64)]
+    return lab[:, src(raw.shape[1], H)][:, :, src(raw.shape[2], W)].astype(np.int32)
+
+
 def resize_bilinear_ac(x, h_out: int, w_out: int):
     """align_corners bilinear with TF's arithmetic form:
     top = tl + (tr-tl)*xl; bottom = bl + (br-bl)*xl; out = top + (bottom-top)*yl."""

@@ -1,0 +1,56 @@
+"""Device input preprocessing (csrc/input.hip) against the oracle's
+restatement, bit-exact for images and labels (the kernel divides its scales on the host and
+keeps FMA contraction off, as TF's CPU resize rounds); and the TFRecord -> PNG -> device batch
+path end to end."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+L2C = [-1] * 7 + list(range(19)) + [-1] * 8
+
+
+@pytest.mark.parametrize("src,dst", [((37, 53), (64, 96)), ((100, 200), (48, 64)),
+                                     ((64, 128), (64, 128)), ((1024, 2048), (512, 1024))])
+def test_prepare_images_and_labels(cuda, src, dst):
+    from input_pipelines.tfrecords import prepare_images, prepare_labels
+    from oracle.tfseg import prepare_images_np, prepare_labels_np
+    rng = np.random.default_rng(sum(src) + sum(dst))
+    raw = rng.integers(0, 256, (2,) + src + (3,), dtype=np.uint8)
+    lab = rng.integers(0, 34, (2,) + src, dtype=np.uint8)
+    im = prepare_images(torch.from_numpy(raw).to(cuda), *dst).cpu().numpy()
+    la = prepare_labels(torch.from_numpy(lab).to(cuda), *dst, L2C).cpu().numpy()
+    ref_i = prepare_images_np(raw, *dst)
+    np.testing.assert_array_equal(im, ref_i)
+    np.testing.assert_array_equal(la, prepare_labels_np(lab, *dst, L2C))
+
+
+def test_prepare_labels_out_of_table_ids(cuda):
+    from input_pipelines.tfrecords import prepare_labels
+    lab = torch.tensor([[[0, 40], [33, 255]]], dtype=torch.uint8, device=cuda)
+    out = prepare_labels(lab, 2, 2, L2C).cpu().numpy()
+    assert out.tolist() == [[[19, -1], [19, -1]]]
+
+
+def test_tfrecord_input_end_to_end(cuda, tmp_path):
+    from input_pipelines.tfrecords import (encode_example, encode_png, tfrecord_input,
+                                           write_records)
+    from oracle.tfseg import prepare_images_np, prepare_labels_np
+    rng = np.random.default_rng(7)
+    ims = rng.integers(0, 256, (4, 40, 80, 3), dtype=np.uint8)
+    las = rng.integers(0, 34, (4, 40, 80), dtype=np.uint8)
+    recs = [encode_example({"image/encoded": [encode_png(ims[i])],
+                            "label/encoded": [encode_png(las[i])],
+                            "image/path": [f"im{i}.png".encode()],
+                            "label/path": [f"la{i}.png".encode()]}) for i in range(4)]
+    p = str(tmp_path / "eval.tfrecord")
+    write_records(p, recs)
+    batches = list(tfrecord_input(p, L2C, 32, 64, nb=2))
+    assert len(batches) == 2
+    for b, (f, l) in enumerate(batches):
+        ref_i = prepare_images_np(ims[2 * b:2 * b + 2], 32, 64)
+        np.testing.assert_array_equal(f["proimages"].cpu().numpy(), ref_i)
+        np.testing.assert_array_equal(l["prolabels"].cpu().numpy(),
+                                      prepare_labels_np(las[2 * b:2 * b + 2], 32, 64, L2C))
+        assert f["rawimagespaths"] == [f"im{2 * b}.png".encode(), f"im{2 * b + 1}.png".encode()]
