@@ -5,7 +5,7 @@ Same command line: ``python evaluate.py <log_dir> <Neval> <training_problem_def_
 [--replace_voids] [--Nb N]`` plus the model flags. The reference's own ``__main__`` raises
 NotImplementedError (evaluate.py:81-83); here ``main`` runs: checkpoints written by train.py
 (``<log_dir>/model.ckpt-<step>.pt``) are evaluated on the eval input_fn (seeded synthetic
-Cityscapes-shaped batches: the TFRecord reader is out of scope), the confusion matrices are
+Cityscapes-shaped batches, or ``--tfrecords_path`` TFRecords of KEYS2FEATURES_v5 examples), the confusion matrices are
 accumulated on the device and printed / saved like evaluate.py:56-68 (``all_metrics.txt``;
 the raw metrics as ``all_metrics.npz`` instead of a pickle).
 """
@@ -23,6 +23,16 @@ from system_factory import SemanticSegmentation  # noqa: E402
 from utils.utils import SemanticSegmentationArguments, print_metrics_from_confusion_matrix  # noqa: E402
 
 
+def tfrecord_eval_fn(config, params):
+    """evaluate_input over params.tfrecords_path (input_cityscapes.py:190-240): TFRecord ->
+    PNG decode on the host, resize / lids2cids (evaluation problem definition) on the device."""
+    from input_pipelines.tfrecords import tfrecord_input
+    from input_pipelines.utils import get_temp_Nb
+    return tfrecord_input(params.tfrecords_path, params.evaluation_problem_def['lids2cids'],
+                          params.height_feature_extractor, params.width_feature_extractor,
+                          get_temp_Nb(config, params.Nb))
+
+
 def _add_extra_args(args):
     # evaluate.py:70-79: no regularizer, batch-norm decay irrelevant in inference
     args.regularization_weight = 0.0
@@ -35,9 +45,12 @@ def main(argv, max_steps=None):
     ssargs.argparser.add_argument('per_pixel_dataset_name', type=str,
                                   choices=['vistas', 'cityscapes'])
     ssargs.argparser.add_argument('--eval_res_dir', type=str, default=None)
+    # the reference hard-codes its TFRecord path; without one, seeded synthetic batches
+    ssargs.argparser.add_argument('--tfrecords_path', type=str, default=None)
     args = ssargs.parse_args(argv)
     _add_extra_args(args)
-    system = SemanticSegmentation({'eval': eval_fn}, model_fn, args)
+    system = SemanticSegmentation({'eval': tfrecord_eval_fn if args.tfrecords_path else eval_fn},
+                                  model_fn, args)
     all_metrics = system.evaluate(max_steps=max_steps)
     s = system.settings
     labels = s.evaluation_problem_def['cids2labels']

