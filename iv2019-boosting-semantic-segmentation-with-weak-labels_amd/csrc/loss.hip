@@ -509,6 +509,14 @@ __global__ __launch_bounds__(256) void eval_decisions_kernel(EvalArgs a, LossTab
     a.out[id] = d;
   }
 }
+__global__ void confusion_global_kernel(const int* __restrict__ lab, const int* __restrict__ dec,
+                                        long n, int nc, int* cm) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int l = lab[i], d = dec[i];
+    if (l >= 0 && l < nc && d >= 0 && d < nc) atomicAdd(&cm[l * nc + d], 1);
+  }
+}
+
 }  // namespace
 
 int loss_head_blocks(int N, int Hl, int Wl) {
@@ -536,8 +544,14 @@ hipError_t launch_loss_finalize(const float* part, int nblocks, const LossTables
 
 hipError_t launch_confusion(const int* labels, const int* decisions, long n, int num_classes,
                             int* cm, hipStream_t s) {
-  if (num_classes > 64) return hipErrorInvalidValue;
+  if (num_classes <= 0 || num_classes > 256) return hipErrorInvalidValue;
   long g = (n + 255) / 256;
+  if (num_classes > 64) {   // Vistas (66 classes): the histogram does not fit the LDS tile
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(confusion_global_kernel, dim3((int)g), dim3(256), 0, s, labels, decisions,
+                       n, num_classes, cm);
+    return hipGetLastError();
+  }
   if (g > 1024) g = 1024;
   hipLaunchKernelGGL(confusion_kernel, dim3((int)g), dim3(256), 0, s, labels, decisions, n,
                      num_classes, cm);

@@ -222,3 +222,18 @@ def test_evaluate_script_main(cuda, tmp_path):
     z = np.load(tmp_path / "eval" / "all_metrics.npz")
     assert z["confusion_matrix"].shape == (1, 19, 19)
 
+
+
+def test_confusion_more_than_64_classes(cuda):
+    """Vistas evaluates 66 classes: the confusion matrix takes the global-atomic path."""
+    cfg = CFGS[0]
+    ctx = _ctx(cfg)
+    rng = np.random.default_rng(4)
+    lab = rng.integers(-1, 67, 100000).astype(np.int32)
+    dec = rng.integers(0, 66, 100000).astype(np.int32)
+    for nc in (20, 66):
+        cm = torch.empty((nc, nc), dtype=torch.int32, device=cuda)
+        ctx.confusion(torch.from_numpy(lab).to(cuda), torch.from_numpy(dec).to(cuda), nc, cm)
+        ok = (lab >= 0) & (lab < nc) & (dec < nc)
+        np.testing.assert_array_equal(cm.cpu().numpy(), confusion_matrix(lab[ok], dec[ok], nc))
+    ctx.close()
