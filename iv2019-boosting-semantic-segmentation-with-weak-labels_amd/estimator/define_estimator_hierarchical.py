@@ -142,20 +142,27 @@ def _eval_spec(predictions, labels, config, params):
 
 
 def _predict_spec(predictions, features, params):
-    """PREDICT branch (define_estimator_hierarchical.py:202-232): decisions mapped to the
-    inference cids (optionally void-replaced) at network resolution; the low-resolution
-    logits stand in for the full-resolution probabilities (softmax of their align-corners
-    upsampling, which the fused head never materialises)."""
+    """PREDICT branch (define_estimator_hierarchical.py:203-238): decisions in TRAINING cids
+    (the reference leaves the inference-cid mapping commented out, :226-227), resized to
+    (height_system, width_system) when both are set, else to the raw image size, else kept at
+    network resolution (_resize_predictions, nearest align-corners); --replace_voids runs on
+    the device only where that resize is the identity (the reference replaces voids on
+    bilinearly resized probabilities). The low-resolution logits stand in for the
+    full-resolution probabilities, which the fused head never materialises."""
     import torch
     ctx = predictions['_context']
-    n = features['proimages'].shape[0]
-    decs = torch.empty((n, params.height_network if hasattr(params, 'height_network')
-                        else params.height_feature_extractor,
-                        params.width_network if hasattr(params, 'width_network')
-                        else params.width_feature_extractor),
-                       dtype=torch.int32, device=features['proimages'].device)
-    ctx.predict(list(params.training_cids2inference_cids), decs,
-                replace_voids=bool(getattr(params, 'replace_voids', False)))
+    img = features['proimages']
+    n, h_net, w_net = img.shape[0], img.shape[1], img.shape[2]
+    size = (getattr(params, 'height_system', None), getattr(params, 'width_system', None))
+    if not all(size):
+        raw = features.get('rawimages')
+        size = (int(raw.shape[1]), int(raw.shape[2])) if raw is not None else (h_net, w_net)
+    replace = bool(getattr(params, 'replace_voids', False))
+    if replace and tuple(size) != (h_net, w_net):
+        raise NotImplementedError('replace_voids with a prediction size different from the '
+                                  'network size (bilinear probability resize) is not built')
+    decs = torch.empty((n,) + tuple(size), dtype=torch.int32, device=img.device)
+    ctx.predict(list(range(params.output_Nclasses)), decs, replace_voids=replace)
     out = {k: v for k, v in predictions.items()
            if k in ('l1_logits', 'l2_vehicle_logits', 'l2_human_logits', '_context')}
     out['decisions'] = decs

@@ -237,3 +237,32 @@ def test_confusion_more_than_64_classes(cuda):
         ok = (lab >= 0) & (lab < nc) & (dec < nc)
         np.testing.assert_array_equal(cm.cpu().numpy(), confusion_matrix(lab[ok], dec[ok], nc))
     ctx.close()
+
+
+def test_predict_script_exports(cuda, tmp_path):
+    """predict.py: images of predict_dir -> device preprocessing -> PREDICT -> decisions at the
+    raw image size exported as label-id / colour / overlapped PNGs (predict.py:112-135)."""
+    import importlib.util
+    from PIL import Image
+    pdir = tmp_path / "in"
+    rdir = tmp_path / "out"
+    pdir.mkdir()
+    rdir.mkdir()
+    rng = np.random.default_rng(6)
+    for i in range(2):
+        Image.fromarray(rng.integers(0, 256, (50, 90, 3), dtype=np.uint8)).save(pdir / f"img{i}.png")
+    path = os.path.join(REPO, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
+                        "predict.py")
+    spec = importlib.util.spec_from_file_location("seg_predict_main", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    n = mod.main([str(tmp_path), PROBLEM, str(pdir), "cityscapes", "--Nb", "1",
+                  "--height_feature_extractor", "48", "--width_feature_extractor", "64",
+                  "--compute_dtype", "fp32", "--results_dir", str(rdir), "--export_lids_images",
+                  "--export_color_decisions", "--export_overlapped_color_decisions"])
+    assert n == 2
+    for i in range(2):
+        lids = np.asarray(Image.open(rdir / f"img{i}_result_lids.png"))
+        col = np.asarray(Image.open(rdir / f"img{i}_result_color.png"))
+        assert lids.shape == (50, 90) and col.shape == (50, 90, 3)
+        assert (rdir / f"img{i}_result_overlapped_color.png").exists()
