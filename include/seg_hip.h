@@ -107,6 +107,8 @@ int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions,
  * seg_set_bn_inference(ctx, 1): later seg_forward calls normalise with the moving statistics
  * (tf.contrib.layers.batch_norm is_training = batch_norm_accumulate_statistics = False,
  * models/resnet50_extended_model_hierarchical.py:40-49,306-307); 0 restores training BN.
+ * Turning it on snapshots the bound buffers (call it again after seg_bind_buffers); the
+ * statistics of every layer are then set by one launch at the start of each forward.
  * seg_predict: decisions of the last seg_forward at out_h x out_w: fused hierarchical argmax
  * (hierarchical.py:88-130) -> cid_map[n_map] (training -> evaluation/inference cids, -1 =
  * void -> max+1; _map_predictions_to_new_cids :490-522) -> optional _replace_voids

@@ -53,6 +53,9 @@ hipError_t launch_bn_stats_finalize(const float* tile_part, long M, int C, int t
 // cross-replica BN: the replica-summed pack -> global mean / biased variance in st
 hipError_t launch_bn_sync_unpack(const float* pack, int C, float inv_world, const float* gamma,
                                  BnState st, hipStream_t s);
+// inference mode, every layer in one launch (one workgroup per job)
+struct BnInferJob { const float* mov_mean; const float* mov_var; const float* gamma; BnState st; int C; };
+hipError_t launch_bn_infer_finalize_all(const BnInferJob* jobs, int n, hipStream_t s);
 // inference mode: st from the moving statistics (no batch statistics)
 hipError_t launch_bn_infer_finalize(const float* mov_mean, const float* mov_var, int C,
                                     const float* gamma, BnState st, hipStream_t s);

@@ -193,6 +193,17 @@ __global__ void bn_infer_finalize_kernel(const float* __restrict__ mov_mean,
   st.var_unb[c] = mov_var[c];
 }
 
+__global__ void bn_infer_finalize_all_kernel(const BnInferJob* __restrict__ jobs) {
+  const BnInferJob j = jobs[blockIdx.x];
+  for (int c = threadIdx.x; c < j.C; c += blockDim.x) {
+    const float inv = rsqrtf(j.mov_var[c] + SEG_BN_EPS);
+    j.st.mean[c] = j.mov_mean[c];
+    j.st.invstd[c] = inv;
+    j.st.scale[c] = j.gamma[c] * inv;
+    j.st.var_unb[c] = j.mov_var[c];
+  }
+}
+
 // ---- forward apply ---------------------------------------------------------------------
 template <typename T, typename TO, int VEC>
 __global__ void bn_apply_kernel(BnApplyArgs a) {
@@ -780,6 +791,12 @@ hipError_t launch_bn_sync_unpack(const float* pack, int C, float inv_world, cons
                                  BnState st, hipStream_t s) {
   hipLaunchKernelGGL(bn_sync_unpack_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, s, pack, C,
                      inv_world, gamma, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_infer_finalize_all(const BnInferJob* jobs, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bn_infer_finalize_all_kernel, dim3(n), dim3(256), 0, s, jobs);
   return hipGetLastError();
 }
 

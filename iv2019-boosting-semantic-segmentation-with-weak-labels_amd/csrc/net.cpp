@@ -158,6 +158,7 @@ struct seg_ctx {
   // cross-replica BN (seg_set_bn_sync): per-layer moment exchange through the caller's hook
   seg_allreduce_fn sync_fn = nullptr;
   int bn_infer = 0;   // seg_set_bn_inference: forward normalises with the moving statistics
+  BnInferJob* infer_jobs = nullptr;   // device table: every layer's moving stats -> BnState
   void* sync_user = nullptr;
   int sync_world = 1;
   float* sync_pack = nullptr;     // [2 * max C]
@@ -441,12 +442,8 @@ int conv_forward(Step& S, int li, const Act& x) {
   if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
   HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
-  if (c->bn_infer) {   // is_training=False: the moving statistics normalise (no exchange)
-    const long half = c->n_moving / 2;
-    HIPCALL(c, launch_bn_infer_finalize(c->moving + L.mv_off, c->moving + half + L.mv_off, L.co,
-                                        c->params + L.g_off, L.st, S.s));
-    return 0;
-  }
+  if (c->bn_infer) return 0;   // is_training=False: the statistics were set for every layer
+                               // by one launch at the start of the forward
   const bool sync = c->sync_fn != nullptr;
   HIPCALL(c, launch_bn_stats_finalize(L.stats_part, M, L.co, conv_nt_stat_rows(S.dt, 0, a), c->stat_scratch,
                                       c->params + L.g_off, L.st, S.s, sync ? c->sync_pack : nullptr));
@@ -994,6 +991,8 @@ Act logits_slice(seg_ctx* c, int h) {
 
 int forward(Step& S, const float* images) {
   seg_ctx* c = S.c;
+  if (c->bn_infer)
+    HIPCALL(c, launch_bn_infer_finalize_all(c->infer_jobs, (int)c->convs.size(), S.s));
   if (c->stem8) {
     HIPCALL(c, launch_cast_pad8(S.dt, images, c->img.p, c->img.M(), S.s));
   } else {
@@ -1201,6 +1200,7 @@ int seg_destroy(seg_ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   for (void* p : c->allocs) (void)hipFree(p);
+  if (c->infer_jobs) (void)hipFree(c->infer_jobs);
   for (auto ev : c->prof.ev) (void)hipEventDestroy(ev);
   for (auto ev : c->bk_ev) (void)hipEventDestroy(ev);
   for (auto ev : c->ev_dy) (void)hipEventDestroy(ev);
@@ -1306,6 +1306,19 @@ int seg_loss(seg_ctx* c, const int32_t* px, const float* bbox, const float* tag,
 
 int seg_set_bn_inference(seg_ctx* c, int on) {
   if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (on) {   // (re)build the per-layer job table from the bound buffers (outside any step)
+    NEED_BOUND(c);
+    std::vector<BnInferJob> jobs;
+    const long half = c->n_moving / 2;
+    for (const ConvL& L : c->convs)
+      jobs.push_back({c->moving + L.mv_off, c->moving + half + L.mv_off, c->params + L.g_off,
+                      L.st, L.co});
+    if (!c->infer_jobs) {
+      HIPCALL(c, hipMalloc(&c->infer_jobs, jobs.size() * sizeof(BnInferJob)));
+    }
+    HIPCALL(c, hipMemcpy(c->infer_jobs, jobs.data(), jobs.size() * sizeof(BnInferJob),
+                         hipMemcpyHostToDevice));
+  }
   c->bn_infer = on ? 1 : 0;
   return 0;
 }
