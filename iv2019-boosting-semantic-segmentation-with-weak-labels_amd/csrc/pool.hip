@@ -55,6 +55,45 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W,
 
 // gather form: each input pixel sums the gradients of the (<= 4) windows whose stored first
 // max (forward argmax byte) is this pixel — no atomics, no recomputation
+// C = 64 (the stem pool): blockIdx.y is one input row (n, hi) so the row decode is scalar;
+// a thread owns 8 channels of one input pixel (8 threads per pixel, 128 B per pixel)
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_row_kernel(
+    const uint8_t* __restrict__ arg, int H, int W, const T* __restrict__ dy, int Ho, int Wo,
+    int lddy, T* __restrict__ dx, int lddx, int ph, int pw) {
+  constexpr int C = 64;
+  const int n = blockIdx.y / H, hi = blockIdx.y - n * H;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= W * 8) return;
+  const int wi = idx >> 3, cg = idx & 7;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const int ho_lo = hi + ph - 2 < 0 ? 0 : (hi + ph - 1) >> 1;
+  const int ho_hi = (hi + ph) >> 1;
+  const int wo_lo = wi + pw - 2 < 0 ? 0 : (wi + pw - 1) >> 1;
+  const int wo_hi = (wi + pw) >> 1;
+  for (int ho = ho_lo; ho <= ho_hi && ho < Ho; ++ho) {
+    for (int wo = wo_lo; wo <= wo_hi && wo < Wo; ++wo) {
+      const size_t q = (size_t)((long)n * Ho + ho) * Wo + wo;
+      const uint2 a = *(const uint2*)(arg + q * C + cg * 8);
+      const uint32_t me = (uint32_t)((hi - (ho * 2 - ph)) * 3 + (wi - (wo * 2 - pw)));
+      uint32_t b[8] = {a.x & 255, (a.x >> 8) & 255, (a.x >> 16) & 255, a.x >> 24,
+                       a.y & 255, (a.y >> 8) & 255, (a.y >> 16) & 255, a.y >> 24};
+      bool any = false;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) any |= b[e] == me;
+      if (!any) continue;
+      float g[8];
+      Vec8<T>::load(dy + q * lddy + cg * 8, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (b[e] == me) acc[e] += g[e];
+    }
+  }
+  Vec8<T>::store(dx + ((size_t)((long)n * H + hi) * W + wi) * lddx + cg * 8, acc);
+}
+
 template <typename T>
 __global__ void maxpool_bwd_kernel(const uint8_t* __restrict__ arg, int N, int H, int W, int C,
                                    const T* __restrict__ dy, int Ho, int Wo, int lddy,
@@ -362,6 +401,19 @@ hipError_t launch_maxpool_bwd(int dtype, const void* arg, int N, int H, int W, i
                               int pad_h, int pad_w, hipStream_t s) {
   if (C % 8 || lddy % 8 || lddx % 8) return hipErrorInvalidValue;
   if ((long)N * H * W * C / 8 >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit decode
+  if (C == 64 && (long)N * H < 65536) {   // the stem pool: one row of the input per grid row
+    dim3 g((unsigned)ceil_div((long)W * 8, 256), (unsigned)(N * H));
+    if (dtype == SEG_BF16)
+      hipLaunchKernelGGL(maxpool_bwd_row_kernel<bf16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, H, W,
+                         (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx, pad_h, pad_w);
+    else if (dtype == SEG_F16)
+      hipLaunchKernelGGL(maxpool_bwd_row_kernel<f16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, H, W,
+                         (const f16_t*)dy, Ho, Wo, lddy, (f16_t*)dx, lddx, pad_h, pad_w);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_row_kernel<float>, g, dim3(256), 0, s, (const uint8_t*)arg, H, W,
+                         (const float*)dy, Ho, Wo, lddy, (float*)dx, lddx, pad_h, pad_w);
+    return hipGetLastError();
+  }
   dim3 g(grid_for((long)N * H * W * C / 8));
   if (dtype == SEG_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, N, H, W,
