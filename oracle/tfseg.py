@@ -378,6 +378,25 @@ CITYSCAPES = dict(
 )
 
 
+# Vistas: define_losses_hierarchical.py:38-74 (label remaps) and
+# models/resnet50_extended_model_hierarchical.py:95-106 (decision fusion), as listed there
+VISTAS = dict(
+    cid_l1_vehicle=49, cid_l1_human=19,
+    pp2l1=list(range(20)) + [19, 19, 19] + list(range(20, 50)) + [49] * 10 + [50, 51, 52],
+    pb2l1=[49, 49, 49, 49, 49, 49, 19, 19, 19, 19, 19, 52, 52, 52, 52],
+    pp2veh=[11] * 52 + list(range(11)) + [11, 11, 11],
+    pb2veh=[0, 2, 3, 5, 6, 9, 11, 11, 11, 11, 11, 11, 11, 11, 11],
+    pp2hum=[4] * 19 + [0, 1, 2, 3] + [4] * 43,
+    pb2hum=[4, 4, 4, 4, 4, 4, 0, 0, 0, 0, 0, 4, 4, 4, 4],
+    l1_to_common=list(range(20)) + list(range(23, 53)) + [63, 64, 65],
+    veh_to_common=[52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 65],
+    hum_to_common=[19, 20, 21, 22, 65],
+)
+assert len(VISTAS["pp2l1"]) == 66 and len(VISTAS["pp2veh"]) == 66 and len(VISTAS["pp2hum"]) == 66
+assert len(VISTAS["l1_to_common"]) == 53
+TABLES = {"cityscapes": CITYSCAPES, "vistas": VISTAS}
+
+
 def _t(v):
     return torch.as_tensor(v, dtype=torch.long)
 
@@ -488,7 +507,7 @@ class OracleNet:
               for k in ("l1_logits", "l2_vehicle_logits", "l2_human_logits")}
         probs = {k: torch.softmax(v, dim=1) for k, v in up.items()}
         decs = {k: torch.argmax(v, dim=1) for k, v in probs.items()}
-        t = CITYSCAPES
+        t = TABLES[cfg.dataset]
         l1d, vd, hd = decs["l1_logits"], decs["l2_vehicle_logits"], decs["l2_human_logits"]
         fused = torch.where(l1d == t["cid_l1_vehicle"], _t(t["veh_to_common"])[vd],
                             torch.where(l1d == t["cid_l1_human"], _t(t["hum_to_common"])[hd],
@@ -521,7 +540,7 @@ class OracleNet:
     # -- losses (define_losses_hierarchical.py:98-210) ---------------------------------
     def losses(self, low, px_labels, bbox_soft=None, tag_soft=None):
         cfg = self.cfg
-        t = CITYSCAPES
+        t = TABLES[cfg.dataset]
         up, probs, decs, _ = self.head_predictions(low)
         npp = cfg.nb_pp
         lab = torch.as_tensor(px_labels, dtype=torch.long)
