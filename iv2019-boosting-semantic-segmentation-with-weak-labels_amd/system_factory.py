@@ -217,9 +217,16 @@ class SemanticSegmentation(object):
         if not ckpt_path:
             ck = sorted(glob.glob(join(s.log_dir, 'model.ckpt-*.pt')),
                         key=lambda p: int(re.findall(r'-(\d+)\.pt$', p)[0]))
+            if not ck:   # TF V2 checkpoints (the reference's Saver layout)
+                ck = [p[:-len('.index')] for p in sorted(
+                    glob.glob(join(s.log_dir, 'model.ckpt-*.index')),
+                    key=lambda p: int(re.findall(r'-(\d+)\.index$', p)[0]))]
             ckpt_path = ck[-1] if ck else None
         if not ckpt_path:
             return 0
+        if exists(ckpt_path + '.index'):
+            from utils.tf_checkpoint import import_checkpoint
+            return import_checkpoint(ctx, ckpt_path, momentum=False)
         state = torch.load(ckpt_path, weights_only=True)
         # restore_emas: evaluate the shadow (EMA) weights when asked and present
         params = state.get('ema') if getattr(s, 'restore_emas', False) and 'ema' in state \

@@ -66,3 +66,30 @@ def test_warm_start_from_slim_names(cuda, tmp_path):
         else:
             np.testing.assert_array_equal(after[p.name], before[p.name])
     ctx.close()
+
+
+def test_evaluate_restores_tf_checkpoint(cuda, tmp_path):
+    """SemanticSegmentation.evaluate() picks up a TF-format checkpoint in log_dir (the
+    reference's Saver layout) when no native one exists."""
+    import os
+    from input_pipelines.synthetic import evaluate_input
+    from models.initializers import init_params
+    from models.resnet50_extended_model_hierarchical import add_model_arguments, model
+    from system_factory import SemanticSegmentation
+    from utils.tf_checkpoint import export_checkpoint
+    from utils.utils import SemanticSegmentationArguments
+    from estimator.mode_keys import ModeKeys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prob = os.path.join(repo, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
+                        "problem_definitions", "cityscapes", "problem01.json")
+    src = _ctx(height=48, width=64, pyramid="none")
+    src.load_params(init_params(src.param_info, seed=11))
+    export_checkpoint(src, str(tmp_path / "model.ckpt-77"), 77)
+    a = SemanticSegmentationArguments(mode=ModeKeys.EVAL)
+    add_model_arguments(a.argparser)
+    s = a.parse_args([str(tmp_path), "1", prob, "--Nb", "1", "--height_feature_extractor", "48",
+                      "--width_feature_extractor", "64", "--compute_dtype", "fp32"])
+    s.per_pixel_dataset_name = "cityscapes"
+    res = SemanticSegmentation({"eval": evaluate_input}, model, s).evaluate()
+    assert res[0]["global_step"] == 77
+    src.close()
