@@ -176,7 +176,7 @@ int seg_bbox_labels(const float* boxes, const int32_t* cids, const int32_t* box_
                     void* stream);
 int seg_tag_labels(const float* tags, int n, int H, int W, float* out, void* stream);
 
-/* internal tensors for parity tests: "logits", "grad_un", "dzscale", "feat", "dfeat",
+/* internal tensors for parity tests: "logits", "grad_un", "dzscale", "feat", "dfeat", "z0",
  * "head<h>_out", "head<h>_dout", "conv<i>_x" (input of the last forward), "conv<i>_y",
  * "conv<i>_dy" (i = creation index).
  * dims = N, H, W, C; ld = pixel stride; dtype = SEG_DTYPE_* of the storage */

@@ -1513,6 +1513,7 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
   else if (n == "dzscale") { a.p = c->dzscale; a.N = a.H = a.W = 1; a.C = a.ld = c->ldl; dt = SEG_DTYPE_F32; }
   else if (n == "feat") a = c->feat;
   else if (n == "dfeat") a = c->dfeat;
+  else if (n == "z0") a = c->z0;   // stem BN + ReLU output (the max-pool input)
   else if (n.rfind("head", 0) == 0 && n.size() > 5) {
     int h = n[4] - '0';
     if (h < 0 || h > 2) return set_err(&c->err, -EINVAL, "bad head");

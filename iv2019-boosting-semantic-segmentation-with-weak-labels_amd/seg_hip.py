@@ -340,6 +340,22 @@ class SegContext:
             t = _wrap_u16(ptr.value, (n * hh * ww, ld.value), self.device, half=dt.value == 2)
         return t[:, :c].float().cpu().numpy().reshape(n, hh, ww, c)
 
+    def debug_device(self, name: str):
+        """Zero-copy device view [N,H,W,C] (storage dtype, pixel stride ld) of an internal
+        tensor: the full-size parity tests read 1024 x 2048 activations without a host copy."""
+        import torch
+        ptr = ctypes.c_void_p()
+        dims = (ctypes.c_int * 4)()
+        ld, dt = ctypes.c_int(), ctypes.c_int()
+        check(LIB.seg_debug_tensor(self.h, name.encode(), ctypes.byref(ptr), dims, ctypes.byref(ld),
+                                   ctypes.byref(dt)), self.h)
+        n, hh, ww, c = list(dims)
+        if dt.value == 0:
+            t = _wrap(ptr.value, (n * hh * ww, ld.value), self.device)
+        else:
+            t = _wrap_u16(ptr.value, (n * hh * ww, ld.value), self.device, half=dt.value == 2)
+        return t[:, :c].unflatten(0, (n, hh, ww))
+
     def profile(self, enable: bool):
         check(LIB.seg_profile(self.h, int(enable)), self.h)
 

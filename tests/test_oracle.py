@@ -227,3 +227,36 @@ def test_oracle_eval_decisions_map_replace_resize():
     d = net.eval_decisions(low, ident, 3, 3)
     from oracle.tfseg import CITYSCAPES
     assert (d == CITYSCAPES["veh_to_common"][3]).all()
+
+
+# ---------------------------------------------------------------- shifted-GEMM conv restatement
+@pytest.mark.parametrize("case", [
+    # N, H, W, Ci, Co, k, stride, rate, explicit_pad
+    (2, 13, 17, 5, 6, 3, 1, 2, False),     # dilated 3x3, ragged
+    (1, 11, 9, 7, 4, 1, 1, 1, False),      # 1x1
+    (2, 18, 22, 3, 5, 3, 2, 1, True),      # conv2d_same stride 2
+    (1, 19, 23, 3, 4, 7, 2, 1, True),      # stem 7x7/2
+    (1, 9, 12, 4, 3, 3, 1, 18, False),     # rate larger than the map (ASPP 18 at small size)
+    (1, 10, 11, 3, 2, 1, 2, 1, False),     # SAME stride 2 (shortcut-style)
+])
+def test_conv_props_match_conv_tf_and_autograd(case):
+    """oracle/conv_props (the full-size GPU tests' float64 restatement) equals conv_tf and its
+    autograd data / weight gradients."""
+    from oracle.conv_props import conv_dgrad, conv_fwd, conv_wgrad, geometry
+    N, H, W, Ci, Co, k, s, r, ep = case
+    spec = tfseg.ConvSpec("t", Ci, Co, k, s, r, explicit_pad=ep)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(N, H, W, Ci, dtype=torch.float64, generator=g)
+    w = torch.randn(Co, k, k, Ci, dtype=torch.float64, generator=g)
+    xt = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    wt = w.clone().requires_grad_(True)
+    y = tfseg.conv_tf(xt, wt, spec)
+    Ho, Wo = geometry(H, W, spec)[:2]
+    assert (Ho, Wo) == tuple(y.shape[2:])
+    dy = torch.randn(y.shape, dtype=torch.float64, generator=g)
+    y.backward(dy)
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    torch.testing.assert_close(conv_fwd(x, w, spec), y.detach().permute(0, 2, 3, 1), rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(conv_dgrad(dyn, w, spec, H, W), xt.grad.permute(0, 2, 3, 1),
+                               rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(conv_wgrad(x, dyn, spec), wt.grad, rtol=1e-12, atol=1e-12)
