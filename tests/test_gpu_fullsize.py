@@ -12,7 +12,7 @@ stem and the transposed-stride dgrad.
   every output element against the oracle's ``conv_tf`` on the CPU (float32 accumulation of
   the same bf16 / fp16 operands; the convolution of ``resnet50_extended_feature_extractor.py:
   25-30`` / ``hierarchical.py:59-64`` at the C2 layer shapes).
-* ``test_c2_step_layerwise`` — one full C2 training step of the native context, then every
+* ``test_step_layerwise_fullsize`` — one full training step (C2, C4, C5) of the native context, then every
   conv's forward output and weight gradient, and the whole backward chain of the data
   gradients (dgrad -> ReLU mask -> BN backward, residual and strided-subsample shortcuts,
   the ASPP transposes, the stem max-pool), against a float64 restatement fed the tensors the
@@ -200,21 +200,42 @@ def _maxpool_bwd(z0, g):
     return acc[:, ph:ph + H, pw:pw + W]
 
 
-def test_c2_step_layerwise(cuda):
+# BASELINE configs at their per-GPU shape (1024 x 2048, 4 images): C2 as the bench runs it;
+# C4 = R101 + pyramid with the 1:2:1 strong : bbox : tag mix in bf16 (covers C3's kernels and
+# adds the weak-label loss head); C5 = the same mix in fp16 with fp32 master gradients under a
+# loss scale of 4096 (the dynamic scaler settles at 8192 on these weights)
+FULL_CONFIGS = [
+    ("C2", 50, "bf16", (4, 0, 0)),
+    ("C4", 101, "bf16", (1, 2, 1)),
+    ("C5", 101, "fp16", (1, 2, 1)),
+]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name,depth,dtype,mix", FULL_CONFIGS, ids=[c[0] for c in FULL_CONFIGS])
+def test_step_layerwise_fullsize(cuda, name, depth, dtype, mix):
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
-    H, W, NB = 1024, 2048, 4
-    cfg = SegConfig(height=H, width=W, nb_pp=NB, pyramid="aspp")
+    H, W = 1024, 2048
+    npp, npb, npi = mix
+    NB = npp + npb + npi
+    cfg = SegConfig(depth=depth, height=H, width=W, nb_pp=npp, nb_pb=npb, nb_pi=npi, pyramid="aspp")
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=2).items()}
-    data = batch(17, NB, 0, 0, H, W)
-    ctx = SegContext(pyramid="aspp", height=H, width=W, nb_pp=NB, dtype="bf16")
+    data = batch(17, npp, npb, npi, H, W)
+    ctx = SegContext(depth=depth, pyramid="aspp", height=H, width=W, nb_pp=npp, nb_pb=npb,
+                     nb_pi=npi, dtype=dtype)
     ctx.load_params(params)
+    if dtype == "fp16":
+        ctx.set_loss_scale(4096.0)
     dec = torch.zeros((NB, H, W), dtype=torch.int32, device=cuda)
     ctx.forward(torch.as_tensor(data["images"]).to(cuda))
-    ctx.loss(torch.as_tensor(data["px"]).to(cuda), None, None, dec)
+    dev = lambda a: None if a is None else torch.as_tensor(a).to(cuda)
+    ctx.loss(dev(data["px"]), dev(data["bbox"]), dev(data["tag"]), dec)
     losses, _, logits = ctx.outputs()
     ctx.backward()
     torch.cuda.synchronize()
+    assert bool(torch.isfinite(ctx.grads).all()), "non-finite gradients"
+    u = ULP[dtype]
     specs = build_specs(cfg)
     idx = {s.name: i for i, s in enumerate(specs)}
     info = {p.name: p for p in ctx.param_info}
@@ -228,8 +249,8 @@ def test_c2_step_layerwise(cuda):
     def DY(i):
         return ctx.debug_device(f"conv{i}_dy").double()
 
-    def Wt(i):   # the weights the step ran with (bf16 copies of the fp32 masters)
-        return torch.as_tensor(params[specs[i].name + "/weights"]).to(cuda).bfloat16().double()
+    def Wt(i):   # the weights the step ran with (16-bit copies of the fp32 masters)
+        return torch.as_tensor(params[specs[i].name + "/weights"]).to(cuda).to(TDT[dtype]).double()
 
     def gamma(i):
         return torch.as_tensor(params[specs[i].name + "/BatchNorm/gamma"], dtype=torch.float64, device=cuda)
@@ -241,7 +262,7 @@ def test_c2_step_layerwise(cuda):
     # ---- every conv: forward output and weight gradient (the stem's 3 real channels of tap8)
     for i, s in enumerate(specs):
         x = X(i)
-        _elementwise(Y(i), conv_fwd(x, Wt(i), s), 2 * ULP["bf16"], 1e-3, f"fwd {s.name}")
+        _elementwise(Y(i), conv_fwd(x, Wt(i), s), 2 * u, 1e-3, f"fwd {s.name}")
         dy = DY(i)
         _elementwise(native_grad(i), conv_wgrad(x, dy, s), 1e-3, 1e-4, f"wgrad {s.name}",
                      absref=conv_wgrad(x.abs(), dy.abs(), s), n_sum=dy[..., 0].numel())
@@ -301,8 +322,8 @@ def test_c2_step_layerwise(cuda):
     idfd = idx["feature_extractor/extension/decrease_fdims"]
     chk(idfd, dz_dfd, X(idx[f"{pm}/Conv_1"]), "ASPP inputs")
     # ---- encoder units, top down, through residual / subsample / projection shortcuts
-    rn = "feature_extractor/base/resnet_v1_50"
-    scopes = [f"{rn}/{u[0]}" for u in resnet_units(50, 8)]
+    rn = f"feature_extractor/base/resnet_v1_{depth}"
+    scopes = [f"{rn}/{unit[0]}" for unit in resnet_units(depth, 8)]
     g_out, out = dgrad(idfd, X(idfd)), X(idfd)
     for k in reversed(range(len(scopes))):
         g_out = unit_chain(scopes[k], g_out, out)
@@ -320,12 +341,13 @@ def test_c2_step_layerwise(cuda):
     for key, c in (("l1_logits", 14), ("l2_vehicle_logits", 7), ("l2_human_logits", 3)):
         low[key] = lg[..., c0:c0 + c].permute(0, 3, 1, 2).contiguous()
         c0 += c
-    L = net.losses(low, data["px"])
+    L = net.losses(low, data["px"], data["bbox"], data["tag"])
     ref = [float(L[k]) for k in ("segmentation", "l1_segmentation", "l2_vehicle_segmentation",
                                   "l2_human_segmentation")]
     lv = losses.cpu().numpy()
     np.testing.assert_allclose(lv[:4], ref, rtol=1e-4)
-    assert tuple(int(v) for v in lv[4:7]) == tuple(L["counts"])
+    for a, b in zip(lv[4:7], L["counts"]):   # weak weights follow the l1 argmax (near-ties)
+        assert abs(int(a) - int(b)) <= (0 if npb + npi == 0 else max(2, 1e-5 * int(b)))
     _, _, _, fused = net.head_predictions(low)
     mism = float((dec.cpu().long() != fused).double().mean())
     assert mism < 1e-5, f"fused decisions differ on {mism:.2e} of the pixels"
