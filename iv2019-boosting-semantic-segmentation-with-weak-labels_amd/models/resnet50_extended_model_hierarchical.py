@@ -62,13 +62,14 @@ def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
         'aspp' if getattr(params, 'aspp_module', False) else 'none')
     dev = torch.cuda.current_device() if device is None else device
     key = (dev, depth, pyramid, params.height_feature_extractor, params.width_feature_extractor,
-           nb_pp, nb_pb, nb_pi, getattr(params, 'compute_dtype', 'bf16'),
-           params.per_pixel_dataset_name, bool(getattr(params, 'cross_replica_norm', False)))
+           nb_pp, nb_pb, nb_pi, getattr(params, 'compute_dtype', 'fp32'),
+           params.per_pixel_dataset_name, bool(getattr(params, 'cross_replica_norm', False)),
+           getattr(params, 'ema_decay', 0) > 0)
     ctx = _CONTEXTS.get(key)
     if ctx is None:
         ctx = SegContext(depth=depth, pyramid=pyramid, height=params.height_feature_extractor,
                          width=params.width_feature_extractor, nb_pp=nb_pp, nb_pb=nb_pb,
-                         nb_pi=nb_pi, dtype=getattr(params, 'compute_dtype', 'bf16'),
+                         nb_pi=nb_pi, dtype=getattr(params, 'compute_dtype', 'fp32'),
                          dataset=params.per_pixel_dataset_name,
                          feature_dims=getattr(params, 'feature_dims_decreased', 256),
                          bn_decay=getattr(params, 'batch_norm_decay', 0.9),
@@ -81,6 +82,14 @@ def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
             ctx.set_bn_sync()
         _CONTEXTS[key] = ctx
     return ctx
+
+
+def release_contexts():
+    """Destroy every cached context (device memory back to the allocator); the next
+    get_context builds a fresh one from the seeded initialisation."""
+    for ctx in _CONTEXTS.values():
+        ctx.close()
+    _CONTEXTS.clear()
 
 
 def model(mode, features, labels, config, params):
@@ -130,5 +139,7 @@ def add_model_arguments(argparser):
     # ASPP: the reference's commented-out _create_aspp_module (hierarchical.py:209-226), built
     # in the PSP call site's 'pyramid_module' scope; mutually exclusive with --psp_module
     a('--aspp_module', action='store_true')
-    a('--compute_dtype', type=str, default='bf16', choices=['bf16', 'fp16', 'fp32'])
+    # default: the reference's fp32 arithmetic; bf16 / fp16 (with fp32 master weights) are the
+    # MI355X-speed options the benchmark configs name (BASELINE C2-C5)
+    a('--compute_dtype', type=str, default='fp32', choices=['bf16', 'fp16', 'fp32'])
     a('--init_seed', type=int, default=0)

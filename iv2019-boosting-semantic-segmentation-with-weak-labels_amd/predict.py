@@ -32,7 +32,10 @@ SUPPORTED_EXTENSIONS = ['png', 'PNG', 'jpg', 'JPG', 'jpeg', 'JPEG', 'ppm', 'PPM'
 
 
 def predict_dir_input(config, params):
-    """predict_input (input_cityscapes.py:248-292): batches of Nb images of predict_dir."""
+    """predict_input (input_cityscapes.py:248-292): batches of Nb images of predict_dir. The
+    reference batches without drop_remainder, so every image is predicted: the context's
+    batch is fixed at Nb, so a short last batch is padded with its last image and
+    'rawimagespaths' lists only the real ones (the export loop zips over it)."""
     import torch
     from PIL import Image
     from input_pipelines.tfrecords import prepare_images
@@ -42,12 +45,14 @@ def predict_dir_input(config, params):
     fnames = []
     for se in SUPPORTED_EXTENSIONS:
         fnames.extend(glob.glob(os.path.join(params.predict_dir, '*.' + se), recursive=True))
-    for i in range(0, len(fnames) - nb + 1, nb):
-        raws = [np.array(Image.open(f).convert('RGB'), dtype=np.uint8) for f in fnames[i:i + nb]]
+    for i in range(0, len(fnames), nb):
+        chunk = fnames[i:i + nb]
+        padded = chunk + [chunk[-1]] * (nb - len(chunk))
+        raws = [np.array(Image.open(f).convert('RGB'), dtype=np.uint8) for f in padded]
         raw = torch.from_numpy(np.stack(raws)).to(dev)
         yield {'proimages': prepare_images(raw, params.height_feature_extractor,
                                            params.width_feature_extractor),
-               'rawimages': raw, 'rawimagespaths': fnames[i:i + nb]}, None
+               'rawimages': raw, 'rawimagespaths': chunk}, None
 
 
 def _add_predict_arguments(argparser):

@@ -52,6 +52,10 @@ class SegCfg(ctypes.Structure):
 
 
 def _load():
+    # torch first: its HIP runtime must be the process's one before libseg_hip.so resolves
+    # libamdhip64 (loading the library first left torch's later device init with
+    # "no ROCm-capable device" on the box)
+    import torch  # noqa: F401
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(
             f"libseg_hip.so not found at {LIB_PATH}: build it with __graft_entry__.build() "

@@ -153,10 +153,12 @@ class SemanticSegmentation(object):
     # ---- checkpoints ---------------------------------------------------------------
     def save(self, ctx, global_step):
         import torch
-        state = {'global_step': global_step, 'params': ctx.named('params'),
-                 'momentum': ctx.named('momentum')}
+        # tensors, not numpy arrays: the checkpoint must load with torch.load(weights_only=True)
+        named = lambda buf: {k: torch.from_numpy(v) for k, v in ctx.named(buf).items()}
+        state = {'global_step': global_step, 'params': named('params'),
+                 'momentum': named('momentum')}
         if ctx.ema is not None:
-            state['ema'] = ctx.named('ema')
+            state['ema'] = named('ema')
         torch.save(state, join(self._settings.log_dir, f'model.ckpt-{global_step}.pt'))
         if getattr(self._settings, 'tf_checkpoints', False):
             # the reference's Saver layout: <log_dir>/model.ckpt-<step>.{index,data-*}
@@ -181,11 +183,13 @@ class SemanticSegmentation(object):
                            psp_module=bool(getattr(self._settings, 'psp_module', False)))
             return
         state = torch.load(ck[-1], weights_only=True)
-        ctx.load_params(state['params'])
-        mom = state['momentum']
-        for p in ctx.param_info:
-            if p.name in mom:
-                ctx.momentum[p.offset:p.offset + p.numel].copy_(torch.as_tensor(mom[p.name]))
+        ctx.load_params(state['params'])   # (also resets the EMA shadows to the weights)
+        for buf, saved in ((ctx.momentum, state['momentum']), (ctx.ema, state.get('ema'))):
+            if buf is None or saved is None:
+                continue
+            for p in ctx.param_info:
+                if p.name in saved:
+                    buf[p.offset:p.offset + p.numel].copy_(torch.as_tensor(saved[p.name]).reshape(-1))
         step.value = int(state['global_step'])
 
     # ---- evaluation / prediction (system_factory.py:148-158,304-412) -------------------
@@ -211,28 +215,41 @@ class SemanticSegmentation(object):
         s.training_cids2inference_cids = s.inference_problem_def.get(
             'training_cids2inference_cids', list(tcids))
 
+    def _checkpoints(self):
+        """Checkpoint paths in log_dir, oldest first: the native ``model.ckpt-<step>.pt``
+        files, else the TF V2 prefixes ``model.ckpt-<step>`` (the reference's Saver layout)."""
+        s = self._settings
+        ck = sorted(glob.glob(join(s.log_dir, 'model.ckpt-*.pt')),
+                    key=lambda p: int(re.findall(r'-(\d+)\.pt$', p)[0]))
+        if not ck:
+            ck = [p[:-len('.index')] for p in sorted(
+                glob.glob(join(s.log_dir, 'model.ckpt-*.index')),
+                key=lambda p: int(re.findall(r'-(\d+)\.index$', p)[0]))]
+        return ck
+
     def _restore_for_eval(self, ctx, ckpt_path):
         import torch
         s = self._settings
         if not ckpt_path:
-            ck = sorted(glob.glob(join(s.log_dir, 'model.ckpt-*.pt')),
-                        key=lambda p: int(re.findall(r'-(\d+)\.pt$', p)[0]))
-            if not ck:   # TF V2 checkpoints (the reference's Saver layout)
-                ck = [p[:-len('.index')] for p in sorted(
-                    glob.glob(join(s.log_dir, 'model.ckpt-*.index')),
-                    key=lambda p: int(re.findall(r'-(\d+)\.index$', p)[0]))]
-            ckpt_path = ck[-1] if ck else None
-        if not ckpt_path:
-            return 0
+            ck = self._checkpoints()
+            if not ck:   # tf.estimator: "Could not find trained model in model_dir"
+                raise ValueError(f'Could not find a trained model (model.ckpt-*.pt or a TF '
+                                 f'model.ckpt-*.index) in log_dir {s.log_dir}')
+            ckpt_path = ck[-1]
+        restore_emas = bool(getattr(s, 'restore_emas', False))
         if exists(ckpt_path + '.index'):
             from utils.tf_checkpoint import import_checkpoint
-            return import_checkpoint(ctx, ckpt_path, momentum=False)
+            return import_checkpoint(ctx, ckpt_path, momentum=False, restore_emas=restore_emas)
+        if not exists(ckpt_path):
+            raise ValueError(f'checkpoint {ckpt_path} not found (neither a .pt file nor a TF '
+                             f'prefix with {ckpt_path}.index)')
         state = torch.load(ckpt_path, weights_only=True)
-        # restore_emas: evaluate the shadow (EMA) weights when asked and present
-        params = state.get('ema') if getattr(s, 'restore_emas', False) and 'ema' in state \
-            else state['params']
+        if restore_emas and 'ema' not in state:
+            raise KeyError(f'--restore_emas: {ckpt_path} holds no EMA shadows (trained with '
+                           f'--ema_decay 0 or --distribute)')
+        params = state['ema'] if restore_emas else state['params']
         ctx.load_params(params)
-        if params is not state['params']:   # EMA excludes the moving statistics
+        if restore_emas:   # the EMA excludes the BN moving statistics (define_savers.py:46)
             ctx.load_params({k: v for k, v in state['params'].items() if 'moving_' in k})
         return int(state['global_step'])
 
@@ -256,8 +273,9 @@ class SemanticSegmentation(object):
             labels_names = labels_names[:-1]
         ckpts = [getattr(s, 'ckpt_path', None)]
         if getattr(s, 'eval_all_ckpts', False):
-            ckpts = sorted(glob.glob(join(s.log_dir, 'model.ckpt-*.pt')),
-                           key=lambda p: int(re.findall(r'-(\d+)\.pt$', p)[0]))
+            ckpts = self._checkpoints()
+            if not ckpts:
+                raise ValueError(f'--eval_all_ckpts: no checkpoints in log_dir {s.log_dir}')
         ctx = get_context(config, s, mode=ModeKeys.EVAL)
         all_metrics = []
         for cp in ckpts:

@@ -379,10 +379,20 @@ def tf_shapes(ctx) -> Dict[str, Tuple[int, ...]]:
     return out
 
 
+EMA_SCOPE = 'exponential_moving_averages/'
+
+
+def ema_name(var: str) -> str:
+    """TF name of a variable's EMA shadow: ExponentialMovingAverage.apply under
+    variable_scope('exponential_moving_averages') (define_estimator_hierarchical.py:96-111),
+    the key predict_saver restores with --restore_emas (define_savers.py:44-47)."""
+    return EMA_SCOPE + var + '/ExponentialMovingAverage'
+
+
 def export_checkpoint(ctx, prefix: str, global_step: int = 0):
     """Saver-style checkpoint of the context: every model variable under its TF name, its
-    Momentum slot (``<var>/Momentum``), the EMA shadows when kept
-    (``<var>/ExponentialMovingAverage``) and ``global_step`` (int64)."""
+    Momentum slot (``<var>/Momentum``), the EMA shadows when kept (``ema_name(var)``) and
+    ``global_step`` (int64)."""
     params, mom = ctx.named('params'), ctx.named('momentum')
     ema = ctx.named('ema') if ctx.ema is not None else {}
     out = {'global_step': np.array(global_step, np.int64)}
@@ -391,26 +401,41 @@ def export_checkpoint(ctx, prefix: str, global_step: int = 0):
         if p.name in mom:
             out[p.name + '/Momentum'] = _tf_layout(p, mom[p.name])
         if p.name in ema:
-            out[p.name + '/ExponentialMovingAverage'] = _tf_layout(p, ema[p.name])
+            out[ema_name(p.name)] = _tf_layout(p, ema[p.name])
     save_checkpoint(prefix, out)
 
 
-def import_checkpoint(ctx, prefix: str, momentum: bool = True) -> int:
-    """Restore a checkpoint written with the model's own variable names (continue training
-    from log_dir): parameters, moving statistics and momentum; returns global_step."""
+def import_checkpoint(ctx, prefix: str, momentum: bool = True, restore_emas: bool = False) -> int:
+    """Restore a checkpoint written with the model's own variable names; returns global_step.
+
+    Training restart (momentum=True): parameters, moving statistics, Momentum slots and, when
+    the context keeps them, the EMA shadows. Evaluation / prediction (momentum=False): with
+    ``restore_emas`` every variable except the BN moving statistics is read from its EMA
+    shadow (predict_saver, define_savers.py:38-66); a missing shadow is an error, as the
+    reference's Saver restore would be."""
     import torch
     shapes = tf_shapes(ctx)
     vals = load_checkpoint(prefix)
-    missing = [n for n in shapes if n not in vals]
+
+    def src(p):
+        if restore_emas and p.kind not in ('moving_mean', 'moving_variance'):
+            return ema_name(p.name)
+        return p.name
+    missing = [src(p) for p in ctx.param_info if src(p) not in vals]
     if missing:
-        raise KeyError(f'{len(missing)} model variables missing from {prefix}: {missing[:3]}')
-    ctx.load_params({p.name: _native_layout(p, vals[p.name]) for p in ctx.param_info})
-    if momentum:
+        raise KeyError(f'{len(missing)} variables missing from {prefix}: {missing[:3]}')
+    ctx.load_params({p.name: _native_layout(p, vals[src(p)]) for p in ctx.param_info})
+
+    def fill(buf, key):
         for p in ctx.param_info:
-            m = vals.get(p.name + '/Momentum')
-            if m is not None:
-                ctx.momentum[p.offset:p.offset + p.numel].copy_(
-                    torch.as_tensor(_native_layout(p, m).reshape(-1).astype(np.float32)))
+            v = vals.get(key(p.name))
+            if v is not None and p.kind not in ('moving_mean', 'moving_variance'):
+                buf[p.offset:p.offset + p.numel].copy_(
+                    torch.as_tensor(_native_layout(p, v).reshape(-1).astype(np.float32)))
+    if momentum:
+        fill(ctx.momentum, lambda n: n + '/Momentum')
+        if ctx.ema is not None:   # after load_params, which reset the shadows to the weights
+            fill(ctx.ema, ema_name)
     return int(vals.get('global_step', 0))
 
 

@@ -20,3 +20,22 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.fail("gpu test run without a visible GPU")
     return torch.device("cuda", 0)
+
+
+@pytest.fixture
+def init_ckpt():
+    """write_ckpt(log_dir, step=0, **SegContext kwargs): a native model.ckpt-<step>.pt of the
+    seeded initial weights (evaluate / predict refuse a log_dir without a checkpoint, like the
+    reference's Estimator)."""
+    def write(log_dir, step=0, seed=0, **kw):
+        import torch
+        from models.initializers import init_params
+        from seg_hip import SegContext
+        ctx = SegContext(**kw)
+        params = {k: torch.from_numpy(v) for k, v in init_params(ctx.param_info, seed=seed).items()}
+        ctx.close()
+        os.makedirs(log_dir, exist_ok=True)
+        torch.save({"global_step": step, "params": params, "momentum": {}},
+                   os.path.join(str(log_dir), f"model.ckpt-{step}.pt"))
+        return params
+    return write

@@ -90,6 +90,91 @@ def test_evaluate_restores_tf_checkpoint(cuda, tmp_path):
     s = a.parse_args([str(tmp_path), "1", prob, "--Nb", "1", "--height_feature_extractor", "48",
                       "--width_feature_extractor", "64", "--compute_dtype", "fp32"])
     s.per_pixel_dataset_name = "cityscapes"
+    from models.resnet50_extended_model_hierarchical import release_contexts
+    release_contexts()   # a fresh context: the restored weights must come from the file
     res = SemanticSegmentation({"eval": evaluate_input}, model, s).evaluate()
     assert res[0]["global_step"] == 77
+    # the weights evaluate() ran with are the exported ones (HWIO -> OHWI on the way back)
+    from models.resnet50_extended_model_hierarchical import _CONTEXTS
+    ctx = next(iter(_CONTEXTS.values()))
+    got, ref = ctx.named("params"), src.named("params")
+    assert all(np.array_equal(got[k], ref[k]) for k in ref)
+    release_contexts()
     src.close()
+
+
+@pytest.mark.parametrize("fmt", ["tf", "pt"])
+def test_restore_emas_selects_the_shadows(cuda, tmp_path, fmt):
+    """--restore_emas (predict_saver, define_savers.py:38-66): every variable except the BN
+    moving statistics comes from its EMA shadow 'exponential_moving_averages/<var>/
+    ExponentialMovingAverage'; without the flag the raw weights are restored."""
+    import os
+    import torch
+    from input_pipelines.synthetic import evaluate_input
+    from models.initializers import init_params
+    from models.resnet50_extended_model_hierarchical import (_CONTEXTS, add_model_arguments,
+                                                             model, release_contexts)
+    from system_factory import SemanticSegmentation
+    from utils.tf_checkpoint import ema_name, export_checkpoint, list_variables
+    from utils.utils import SemanticSegmentationArguments
+    from estimator.mode_keys import ModeKeys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prob = os.path.join(repo, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
+                        "problem_definitions", "cityscapes", "problem01.json")
+    from seg_hip import SegContext
+    src = SegContext(height=48, width=64, nb_pp=1, pyramid="none", dtype="fp32", ema=True)
+    p0 = init_params(src.param_info, seed=11)
+    for p in src.param_info:   # non-trivial moving statistics, so their source is visible
+        if p.kind in ("moving_mean", "moving_variance"):
+            p0[p.name] = p0[p.name] + 0.25
+    src.load_params(p0)
+    src.ema.copy_(src.params * 0.5 + 0.125)   # shadows that differ from every weight
+    if fmt == "tf":
+        export_checkpoint(src, str(tmp_path / "model.ckpt-5"), 5)
+        names = [n for n, _ in list_variables(str(tmp_path / "model.ckpt-5"))]
+        assert ema_name(src.param_info[0].name) in names
+    else:
+        named = lambda b: {k: torch.from_numpy(v) for k, v in src.named(b).items()}
+        torch.save({"global_step": 5, "params": named("params"), "momentum": named("momentum"),
+                    "ema": named("ema")}, tmp_path / "model.ckpt-5.pt")
+    for restore in (False, True):
+        a = SemanticSegmentationArguments(mode=ModeKeys.EVAL)
+        add_model_arguments(a.argparser)
+        s = a.parse_args([str(tmp_path), "1", prob, "--Nb", "1", "--height_feature_extractor", "48",
+                          "--width_feature_extractor", "64", "--compute_dtype", "fp32"] +
+                         (["--restore_emas"] if restore else []))
+        s.per_pixel_dataset_name = "cityscapes"
+        release_contexts()
+        SemanticSegmentation({"eval": evaluate_input}, model, s).evaluate(log_fn=None)
+        ctx = next(iter(_CONTEXTS.values()))
+        got = ctx.named("params")
+        raw, shadow = src.named("params"), src.named("ema")
+        for p in src.param_info:
+            moving = p.kind in ("moving_mean", "moving_variance")
+            exp = raw[p.name] if (moving or not restore) else shadow[p.name]
+            assert np.array_equal(got[p.name], exp), (restore, p.name)
+    release_contexts()
+    src.close()
+
+
+def test_evaluate_without_checkpoint_fails(cuda, tmp_path):
+    """An empty log_dir is an error (tf.estimator: 'Could not find trained model'), not an
+    evaluation of random weights; so is an explicit --ckpt_path that does not exist."""
+    import os
+    from input_pipelines.synthetic import evaluate_input
+    from models.resnet50_extended_model_hierarchical import add_model_arguments, model, release_contexts
+    from system_factory import SemanticSegmentation
+    from utils.utils import SemanticSegmentationArguments
+    from estimator.mode_keys import ModeKeys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prob = os.path.join(repo, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
+                        "problem_definitions", "cityscapes", "problem01.json")
+    for extra in ([], ["--ckpt_path", str(tmp_path / "model.ckpt-9")], ["--eval_all_ckpts"]):
+        a = SemanticSegmentationArguments(mode=ModeKeys.EVAL)
+        add_model_arguments(a.argparser)
+        s = a.parse_args([str(tmp_path), "1", prob, "--Nb", "1", "--height_feature_extractor", "48",
+                          "--width_feature_extractor", "64", "--compute_dtype", "fp32"] + extra)
+        s.per_pixel_dataset_name = "cityscapes"
+        with pytest.raises(ValueError):
+            SemanticSegmentation({"eval": evaluate_input}, model, s).evaluate(log_fn=None)
+    release_contexts()

@@ -154,12 +154,13 @@ def _eval_settings(tmp_path, nb=2, h=64, w=128, neval=4):
     return s
 
 
-def test_evaluate_end_to_end(cuda, tmp_path):
+def test_evaluate_end_to_end(cuda, tmp_path, init_ckpt):
     """SemanticSegmentation.evaluate(): per-batch EVAL specs, device confusion matrices summed
     over the pass, void row/column dropped (system_factory.py:395-405)."""
     from input_pipelines.synthetic import evaluate_input
     from models.resnet50_extended_model_hierarchical import model
     from system_factory import SemanticSegmentation
+    init_ckpt(tmp_path, pyramid="psp", height=64, width=128, nb_pp=2, dtype="fp32")
     s = _eval_settings(tmp_path)
     system = SemanticSegmentation({"eval": evaluate_input}, model, s)
     res = system.evaluate()
@@ -183,7 +184,7 @@ def test_evaluate_end_to_end(cuda, tmp_path):
     assert st.num_eval_steps == 2
 
 
-def test_predict_end_to_end(cuda, tmp_path):
+def test_predict_end_to_end(cuda, tmp_path, init_ckpt):
     from input_pipelines.synthetic import predict_input
     from models.resnet50_extended_model_hierarchical import model
     from system_factory import SemanticSegmentation
@@ -196,6 +197,7 @@ def test_predict_end_to_end(cuda, tmp_path):
                       "--height_feature_extractor", "48", "--width_feature_extractor", "64",
                       "--compute_dtype", "fp32"])
     s.per_pixel_dataset_name = "cityscapes"
+    init_ckpt(tmp_path, pyramid="none", height=48, width=64, nb_pp=1, dtype="fp32")
     system = SemanticSegmentation({"predict": predict_input}, model, s)
     preds = list(system.predict(max_steps=2))
     assert len(preds) == 2
@@ -204,7 +206,7 @@ def test_predict_end_to_end(cuda, tmp_path):
         assert d.shape == (1, 48, 64) and d.min() >= 0 and d.max() <= 19
 
 
-def test_evaluate_script_main(cuda, tmp_path):
+def test_evaluate_script_main(cuda, tmp_path, init_ckpt):
     """evaluate.py main: the reference's command line, metrics written to <log_dir>/eval."""
     import importlib.util
     path = os.path.join(REPO, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
@@ -212,6 +214,7 @@ def test_evaluate_script_main(cuda, tmp_path):
     spec = importlib.util.spec_from_file_location("seg_evaluate_main", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    init_ckpt(tmp_path, pyramid="none", height=48, width=64, nb_pp=1, dtype="fp32")
     res = mod.main([str(tmp_path), "2", PROBLEM, "cityscapes", "--Nb", "1",
                     "--height_feature_extractor", "48", "--width_feature_extractor", "64",
                     "--compute_dtype", "fp32"])
@@ -239,7 +242,7 @@ def test_confusion_more_than_64_classes(cuda):
     ctx.close()
 
 
-def test_predict_script_exports(cuda, tmp_path):
+def test_predict_script_exports(cuda, tmp_path, init_ckpt):
     """predict.py: images of predict_dir -> device preprocessing -> PREDICT -> decisions at the
     raw image size exported as label-id / colour / overlapped PNGs (predict.py:112-135)."""
     import importlib.util
@@ -249,19 +252,21 @@ def test_predict_script_exports(cuda, tmp_path):
     pdir.mkdir()
     rdir.mkdir()
     rng = np.random.default_rng(6)
-    for i in range(2):
+    for i in range(3):
         Image.fromarray(rng.integers(0, 256, (50, 90, 3), dtype=np.uint8)).save(pdir / f"img{i}.png")
+    init_ckpt(tmp_path, pyramid="none", height=48, width=64, nb_pp=2, dtype="fp32")
     path = os.path.join(REPO, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd",
                         "predict.py")
     spec = importlib.util.spec_from_file_location("seg_predict_main", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    n = mod.main([str(tmp_path), PROBLEM, str(pdir), "cityscapes", "--Nb", "1",
+    # 3 images at Nb 2: the short last batch is padded, every image is exported
+    n = mod.main([str(tmp_path), PROBLEM, str(pdir), "cityscapes", "--Nb", "2",
                   "--height_feature_extractor", "48", "--width_feature_extractor", "64",
                   "--compute_dtype", "fp32", "--results_dir", str(rdir), "--export_lids_images",
                   "--export_color_decisions", "--export_overlapped_color_decisions"])
-    assert n == 2
-    for i in range(2):
+    assert n == 3
+    for i in range(3):
         lids = np.asarray(Image.open(rdir / f"img{i}_result_lids.png"))
         col = np.asarray(Image.open(rdir / f"img{i}_result_color.png"))
         assert lids.shape == (50, 90) and col.shape == (50, 90, 3)

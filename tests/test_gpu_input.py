@@ -56,7 +56,7 @@ def test_tfrecord_input_end_to_end(cuda, tmp_path):
         assert f["rawimagespaths"] == [f"im{2 * b}.png".encode(), f"im{2 * b + 1}.png".encode()]
 
 
-def test_evaluate_from_tfrecords(cuda, tmp_path):
+def test_evaluate_from_tfrecords(cuda, tmp_path, init_ckpt):
     """evaluate.py --tfrecords_path: the confusion matrix of the TFRecord batches equals the
     one built from the oracle-preprocessed labels and the native decisions."""
     import importlib.util
@@ -71,6 +71,7 @@ def test_evaluate_from_tfrecords(cuda, tmp_path):
                             "label/encoded": [encode_png(las[i])]}) for i in range(2)]
     p = str(tmp_path / "val.tfrecord")
     write_records(p, recs)
+    init_ckpt(tmp_path, pyramid="none", height=48, width=64, nb_pp=1, dtype="fp32")
     spec = importlib.util.spec_from_file_location("seg_eval_tfr", os.path.join(pkg, "evaluate.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
