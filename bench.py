@@ -10,7 +10,9 @@ hierarchical.py:209-226 -- `--pyramid psp` runs the reference's live PSP module 
 1024x2048 crops, 4 per-pixel-labelled images per GPU, bf16
 storage with fp32 accumulation, synthetic seeded data resident in HBM. One step = forward +
 fused multi-loss head + backward + gradient all-reduce (RCCL, N>1) + fused SGDM/L2/BN
-moving-average update. Weak scaling: 4 images per GPU at every N.
+moving-average update + the EMA of the model variables (N=1: the reference's single-GPU
+default, ema_decay 0.9; distributed runs drop it, as the reference does). Weak scaling: 4
+images per GPU at every N.
 
 Prints ONE JSON line (rank 0) with the metric, a roofline object for the dominant kernel
 class (HIP-event timed inside the timed region) and the CPU baseline (the oracle — a
@@ -29,8 +31,12 @@ sys.path[:0] = [REPO, PKG]
 H, W, NB = 1024, 2048, 4
 # BASELINE.json configs as per-GPU workloads (4 images per GPU; weak scaling). C4/C5 keep the
 # reference's 1 : 2 : 1 pixel : bbox : tag proportion (train.py:62-64); C5 runs fp16 storage
-# with fp32 master weights / gradients and dynamic loss scaling (DynamicLossScaler).
+# with fp32 master weights / gradients and dynamic loss scaling (DynamicLossScaler). C1 is the
+# reference's own CPU-runnable case (R50, no pyramid -- train.py's default -- 512 x 1024,
+# batch 2), run here on the GPU for completeness.
 CONFIGS = {
+    "C1": {"depth": 50, "mix": (2, 0, 0), "hw": (512, 1024), "pyramid": "none",
+           "name": "C1: ResNet-50 dilated OS8"},
     "C2": {"depth": 50, "mix": (4, 0, 0), "name": "C2: ResNet-50 dilated OS8"},
     "C3": {"depth": 101, "mix": (4, 0, 0), "name": "C3: ResNet-101 dilated OS8"},
     "C4": {"depth": 101, "mix": (2, 2, 0), "name": "C4: ResNet-101 dilated OS8, strong + bbox-weak"},
@@ -40,14 +46,21 @@ CONFIGS = {
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_TBS = 8.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
-CLS_NAMES = {0: "conv_nt_kernel (forward implicit GEMM)", 1: "conv_nt_kernel (data-gradient)",
-             2: "conv_wgrad_kernel (weight-gradient, split-K)", 3: "bn_apply (BN + ReLU + residual)",
-             4: "bn_bwd_reduce", 5: "bn_bwd_apply"}
+# the kernels each profiled class launches (rocprofv3 names: conv_nt_pp_kernel for Co > 128,
+# conv_nt_v2_kernel for Co <= 128 and the tap8 stem; conv_wgrad_pp_kernel for 256 x 256 tiles,
+# conv_wgrad_v2_kernel below; fp32 parity mode runs the v1 conv_nt_kernel / conv_wgrad_kernel)
+CLS_NAMES = {0: "conv_nt_pp/v2_kernel (forward implicit GEMM)",
+             1: "conv_nt_pp/v2_kernel (data-gradient)",
+             2: "conv_wgrad_pp/v2_kernel (weight-gradient, split-K)",
+             3: "bn_apply8_kernel (BN + ReLU + residual)", 4: "bn_bwd_reduce8_kernel",
+             5: "bn_bwd_apply8_kernel"}
+EMA_DECAY = 0.9   # utils/utils.py:112 default; off when distributed (system_factory.py:236-238)
 
 
 def cpu_baseline(threads, pyramid):
     """Oracle (PyTorch-CPU fp32 restatement of the TF semantics) on a bounded sample:
-    one 1024x2048 image, one full training step, after a 256x512 warm-up."""
+    one 1024x2048 image, one full training step, after a 256x512 warm-up; plus the C1 shape
+    (the reference's own CPU configuration: R50, no pyramid, 512 x 1024, batch 2, one step)."""
     import numpy as np
     import torch
     from input_pipelines.synthetic import batch
@@ -62,9 +75,18 @@ def cpu_baseline(threads, pyramid):
     t = time.perf_counter()
     net.train_step(d["images"], d["px"])
     dt = time.perf_counter() - t
+    del net
+    c1 = SegConfig(height=512, width=1024, nb_pp=2, pyramid="none")
+    net = OracleNet(c1, init_params(c1), dtype=torch.float32)
+    d = batch(3, 2, 0, 0, 512, 1024)
+    t = time.perf_counter()
+    net.train_step(d["images"], d["px"])
+    d1 = time.perf_counter() - t
     return {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
             "sample": f"1 image 1024x2048, 1 full step (fwd+loss+bwd+SGDM), R50+{pyramid.upper()}, fp32, "
-                      f"oracle/tfseg.py on {threads} host threads ({dt:.1f} s)"}
+                      f"oracle/tfseg.py on {threads} host threads ({dt:.1f} s)",
+            "c1": {"value": round(2.0 / d1, 4), "unit": "images/sec",
+                   "sample": f"C1: R50 (no pyramid) 512x1024 batch 2, 1 full step, fp32 ({d1:.1f} s)"}}
 
 
 def main():
@@ -74,7 +96,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"],
                     help="storage dtype (default: the config's; fp16 for C5, else bf16)")
-    ap.add_argument("--pyramid", default="aspp", choices=["aspp", "psp", "none"])
+    ap.add_argument("--pyramid", default=None, choices=["aspp", "psp", "none"],
+                    help="default: the config's (ASPP as C2-C5 name it; none for C1)")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
                     help="BASELINE.json workload preset (per-GPU share); C2 is the metric's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -99,12 +122,20 @@ def main():
     from models.initializers import init_params
     from seg_hip import SegContext
 
+    global H, W, NB
     cfg = CONFIGS[args.config]
     depth, (nb_pp, nb_pb, nb_pi) = cfg["depth"], cfg["mix"]
+    H, W = cfg.get("hw", (H, W))
+    NB = nb_pp + nb_pb + nb_pi
     if args.dtype is None:
         args.dtype = cfg.get("dtype", "bf16")
+    if args.pyramid is None:
+        args.pyramid = cfg.get("pyramid", "aspp")
+    # the reference's single-GPU step keeps an EMA of the model variables (ema_decay 0.9 with
+    # num_updates = global_step, in UPDATE_OPS); MirroredStrategy runs drop it
+    ema_on = world == 1
     ctx = SegContext(depth=depth, pyramid=args.pyramid, height=H, width=W, nb_pp=nb_pp, nb_pb=nb_pb,
-                     nb_pi=nb_pi, dtype=args.dtype, device=local)
+                     nb_pi=nb_pi, dtype=args.dtype, device=local, ema=ema_on)
     ctx.load_params(init_params(ctx.param_info, seed=0))
     data = batch(1000 + rank, nb_pp, nb_pb, nb_pi, H, W)
     img = torch.as_tensor(data["images"]).to(dev)
@@ -118,12 +149,17 @@ def main():
         from estimator.define_optimizer import DynamicLossScaler
         scaler = DynamicLossScaler(ctx)
 
+    from estimator.define_estimator_hierarchical import ema_decay_effective
+    gstep = [0]
+
     def step():
         ctx.forward(img)
         ctx.loss(px, bbox, tag)
         ctx.backward()
         scale = allreduce_grads(ctx)
-        ctx.apply_update(0.01, 0.9, 0.0, scale)
+        ema = ema_decay_effective(EMA_DECAY, gstep[0]) if ema_on else 0.0
+        ctx.apply_update(0.01, 0.9, ema, scale)
+        gstep[0] += 1
         if scaler is not None:
             scaler.update()   # reads the device overflow flag (one 4-byte copy per step)
 
@@ -187,17 +223,25 @@ def main():
         # HBM bytes per launch of that class from the committed PMC passes of this code
         # (tools/pmc_traffic.sh + tools/pmc_traffic.py; rocprofv3 cannot run inside the bench)
         traffic, tsrc = None, None
-        tpath = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
-        if os.path.exists(tpath):
+        for tname in ("r02_pmc_traffic.json", "r01_pmc_traffic.json"):
+            tpath = os.path.join(REPO, "profiles", tname)
+            if not os.path.exists(tpath):
+                continue
             tj = json.load(open(tpath))
             key = "conv_wgrad" if dom == 2 else "conv_nt"
             if key in tj:
                 traffic = round(tj[key]["hbm_bytes_per_launch"])
-                tsrc = "profiles/r01_pmc_traffic.json (" + key + ", bytes per launch)"
+                tsrc = f"profiles/{tname} ({key}, bytes per launch)"
+                break
         # the north star's named target: the dilated 3x3 convs of the encoder (block3 rate 2,
         # block4 rate 4, and the ASPP rates), per pass, against the MFMA peak
+        dump = ctx.profile_dump()
+        # compulsory HBM bytes per launch of the dominant class (every operand once; for the
+        # weight gradient x + dy in 16 bit and the fp32 dW): traffic / this = re-read factor
+        rows_dom = [row for row in dump if row["cls"] == dom]
+        alg_bytes = sum(row["gbytes"] for row in rows_dom) * 1e9 / max(len(rows_dom), 1)
         dil = {}
-        for row in ctx.profile_dump():
+        for row in dump:
             if row["cls"] <= 2 and row["k"] == 3 and row["rate"] > 1:
                 d = dil.setdefault(row["cls"], [0.0, 0.0, 0])
                 d[0] += row["gflop"]; d[1] += row["ms"]; d[2] += 1
@@ -213,6 +257,8 @@ def main():
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                     "traffic_source": tsrc,
+                    "algorithmic_bytes": round(alg_bytes),
+                    "traffic_ratio": round(traffic / alg_bytes, 3) if traffic and alg_bytes else None,
                     "kernel": CLS_NAMES[dom],
                     "launches": r["launches"],
                     "avg_launch_ms": round(r["ms"] / max(r["launches"], 1), 4),
@@ -280,9 +326,11 @@ def main():
                "ms_per_step": round(elapsed * 1e3 / args.steps, 2),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": args.dtype, "data": "synthetic (seeded; random-init weights)",
+               "ema": EMA_DECAY if ema_on else None,
                "config": {"workload": cfg["name"] + " + " + args.pyramid.upper() +
-                                      ", 1024x2048, multi-loss head (pixel:bbox:tag = %d:%d:%d), "
-                                      "fwd+loss+bwd+allreduce+SGDM" % (nb_pp, nb_pb, nb_pi),
+                                      ", %dx%d, multi-loss head (pixel:bbox:tag = %d:%d:%d), "
+                                      "fwd+loss+bwd+allreduce+SGDM%s" % (H, W, nb_pp, nb_pb, nb_pi,
+                                                                         "+EMA" if ema_on else ""),
                           "global_batch": world * NB, "per_gpu_batch": NB,
                           "image": [H, W], "parallelism": f"dp{world}"},
                "losses_last_step": [round(float(x), 5) for x in lv[:4]],

@@ -187,7 +187,8 @@ int seg_debug_tensor(seg_ctx* ctx, const char* name, void** ptr, int* dims, int*
 int seg_profile(seg_ctx* ctx, int enable);
 int seg_profile_read(seg_ctx* ctx, int cls, double* ms_total, double* gflop_total,
                      int64_t* launches, double* ms_max_layer, char* layer_name, int name_len);
-/* one text line per recorded launch: cls name ci co k rate Ho Wo gflop ms */
+/* one text line per recorded launch: cls name ci co k rate Ho Wo gflop ms gbytes
+ * (gbytes = the launch's compulsory HBM GB: every operand read / written once) */
 int seg_profile_dump(seg_ctx* ctx, char* buf, int len);
 
 /* single-op entry points (parity tests of individual kernels) -------------------------- */

@@ -3,79 +3,12 @@
 #include <cstdlib>
 #include <type_traits>
 
-// BN_NT_STORE (A/B): streaming stores for the apply kernels' outputs
-#ifdef BN_NT_STORE
-#define BN_STORE8(T, p, v) store8_nt<T>(p, v)
-#else
+// (non-temporal stores for the apply kernels' outputs measured no faster)
 #define BN_STORE8(T, p, v) Vec8<T>::store(p, v)
-#endif
 
 namespace {
 
-// ---- forward statistics: merge per-tile (sum, M2) partials with Chan's formula --------
-// stage 1: grid (ceil(C/64), G); block 256 = 64 channels x 4 tile lanes
-constexpr int STAT_TPB = 64;  // tiles per block in stage 1
-
-__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb,
-                                           float m2b) {
-  if (nb <= 0.f) return;
-  if (n <= 0.f) { n = nb; mean = meanb; m2 = m2b; return; }
-  float tot = n + nb;
-  float d = meanb - mean;
-  mean = mean + d * (nb / tot);
-  m2 = m2 + m2b + d * d * (n * nb / tot);
-  n = tot;
-}
-
-__global__ void bn_stats_stage1(const float* __restrict__ part, long M, int C, int tile_rows,
-                                int ntiles, float* __restrict__ out /* [G][C][3] */) {
-  __shared__ float sh[3][4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int tl = threadIdx.x >> 6;
-  const int t0 = blockIdx.y * STAT_TPB;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < C) {
-    for (int t = t0 + tl; t < t0 + STAT_TPB && t < ntiles; t += 4) {
-      long rows = M - (long)t * tile_rows;
-      float nb = (float)(rows < tile_rows ? rows : tile_rows);
-      float2 v = *(const float2*)(part + 2 * ((size_t)t * C + c));
-      chan_merge(n, mean, m2, nb, v.x / nb, v.y);
-    }
-  }
-  sh[0][tl][threadIdx.x & 63] = n;
-  sh[1][tl][threadIdx.x & 63] = mean;
-  sh[2][tl][threadIdx.x & 63] = m2;
-  __syncthreads();
-  if (tl == 0 && c < C) {
-    for (int k = 1; k < 4; ++k)
-      chan_merge(n, mean, m2, sh[0][k][threadIdx.x], sh[1][k][threadIdx.x], sh[2][k][threadIdx.x]);
-    float* o = out + 3 * ((size_t)blockIdx.y * C + c);
-    o[0] = n; o[1] = mean; o[2] = m2;
-  }
-}
-
-__global__ void bn_stats_stage2(const float* __restrict__ g, int G, int C, const float* gamma,
-                                BnState st, float* pack) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int k = 0; k < G; ++k) {
-    const float* o = g + 3 * ((size_t)k * C + c);
-    chan_merge(n, mean, m2, o[0], o[1], o[2]);
-  }
-  float var = m2 / n;
-  float inv = rsqrtf(var + SEG_BN_EPS);
-  st.mean[c] = mean;
-  st.invstd[c] = inv;
-  st.scale[c] = gamma[c] * inv;
-  st.var_unb[c] = m2 / (n > 1.f ? n - 1.f : 1.f);
-  if (pack) {   // this replica's moments for the cross-replica exchange
-    pack[c] = mean;
-    pack[C + c] = var + mean * mean;
-  }
-}
-
-// one-launch finalize of the forward statistics (replaces stage1 + stage2): per-tile (sum, M2)
+// ---- forward statistics: one-launch finalize (a two-launch Chan merge measured slower): per-tile (sum, M2)
 // partials of tile_rows rows (the last one ragged) merged as shifted sums around tile 0's mean
 // p: A = sum_t n_t (mean_t - p), B = sum_t (M2_t + n_t (mean_t - p)^2), so mean = p + A / N and
 // var = B / N - (A / N)^2, with no division per merge; 8 channels x 64 tile lanes per block,
@@ -327,40 +260,6 @@ __global__ void bn_bwd_reduce_kernel(BnBwdArgs a) {
         o[1] = s2[e];
       }
     }
-  }
-}
-
-// block = 8 channels (fast) x 32 row-block lanes; fixed-order float sums, then an LDS tree
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int rb, long M, int C,
-                                       BnState st, float* dgamma, float* dbeta) {
-  __shared__ float sh[2][32][9];
-  const int cl = threadIdx.x & 7, lane = threadIdx.x >> 3;
-  const int c = blockIdx.x * 8 + cl;
-  float s1 = 0.f, s2 = 0.f;
-  if (c < C) {
-    for (int k = lane; k < rb; k += 32) {
-      const float2 v = *(const float2*)(part + 2 * ((size_t)k * C + c));
-      s1 += v.x;
-      s2 += v.y;
-    }
-  }
-  sh[0][lane][cl] = s1;
-  sh[1][lane][cl] = s2;
-  __syncthreads();
-  for (int st2 = 16; st2 > 0; st2 >>= 1) {
-    if (lane < st2) {
-      sh[0][lane][cl] += sh[0][lane + st2][cl];
-      sh[1][lane][cl] += sh[1][lane + st2][cl];
-    }
-    __syncthreads();
-  }
-  if (lane == 0 && c < C) {
-    s1 = sh[0][0][cl];
-    s2 = sh[1][0][cl];
-    st.sdy[c] = s1 / (float)M;
-    st.sdyx[c] = s2 / (float)M;
-    if (dgamma) dgamma[c] = s2;
-    if (dbeta) dbeta[c] = s1;
   }
 }
 
@@ -772,18 +671,9 @@ hipError_t launch_bn_stats_finalize(const float* tile_part, long M, int C, int t
                                     float* scratch, const float* gamma, BnState st,
                                     hipStream_t s, float* pack) {
   int ntiles = ceil_div(M, tile_rows);
-  // A/B: SEG_BN_STATS_2STAGE=1 restores the two-launch Chan merge (stage1 + stage2)
-  static const bool two_stage = getenv("SEG_BN_STATS_2STAGE") && atoi(getenv("SEG_BN_STATS_2STAGE"));
-  if (two_stage) {
-    int G = ceil_div(ntiles, STAT_TPB);
-    hipLaunchKernelGGL(bn_stats_stage1, dim3(ceil_div(C, 64), G), dim3(256), 0, s, tile_part, M, C,
-                       tile_rows, ntiles, scratch);
-    hipLaunchKernelGGL(bn_stats_stage2, dim3(ceil_div(C, 64)), dim3(64), 0, s, scratch, G, C, gamma,
-                       st, pack);
-  } else {
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(ceil_div(C, SF_CH)), dim3(SF_CH * SF_LANES), 0,
-                       s, tile_part, M, C, tile_rows, ntiles, gamma, st, pack);
-  }
+  (void)scratch;
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(ceil_div(C, SF_CH)), dim3(SF_CH * SF_LANES), 0,
+                     s, tile_part, M, C, tile_rows, ntiles, gamma, st, pack);
   return hipGetLastError();
 }
 
@@ -820,8 +710,8 @@ hipError_t launch_bn_apply(int dtype, int out_f32, const BnApplyArgs& a, hipStre
 }
 
 int bn_bwd_rowblocks(long M, int C) {
-  // ~1024 blocks, each >= 64 rows (SEG_BN_RB: A/B of the cap)
-  static const long cap = getenv("SEG_BN_RB") ? atol(getenv("SEG_BN_RB")) : 1024;
+  // ~1024 blocks, each >= 64 rows
+  const long cap = 1024;
   long rb = (M + 63) / 64;
   if (rb > cap) rb = cap;
   (void)C;
@@ -842,13 +732,8 @@ hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipSt
 
 hipError_t launch_bn_bwd_finalize(const float* part, int rb, long M, int C, BnState st,
                                   float* dgamma, float* dbeta, hipStream_t s) {
-  static const int which = getenv("SEG_BN_BWD_FINAL") ? atoi(getenv("SEG_BN_BWD_FINAL")) : 1;
-  if (which == 0)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 8)), dim3(256), 0, s, part, rb, M,
-                       C, st, dgamma, dbeta);
-  else
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ceil_div(C, BF_CH)), dim3(BF_CH * BF_LANES), 0, s,
-                       part, rb, M, C, st, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ceil_div(C, BF_CH)), dim3(BF_CH * BF_LANES), 0, s,
+                     part, rb, M, C, st, dgamma, dbeta);
   return hipGetLastError();
 }
 

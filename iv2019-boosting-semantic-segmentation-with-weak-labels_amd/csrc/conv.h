@@ -28,9 +28,6 @@ struct ConvArgs {
   float* stats;   // BN partials [mtiles][Co] x {sum, M2} (nullptr = none)
   int tap8;       // 1: C == 8 and every 16-B chunk of K is one tap (the 3-channel stem padded
                   // to 8); K = KH*KW*8 is padded to a multiple of 64 with zero weights
-  int grid_cap;   // persistent launches: workgroups <= grid_cap (0 = one per CU)
-  const uint8_t* rmask;   // optional ReLU bits of r ([M][ldm] bytes, bit e = channel 8b+e):
-  int ldm;                // r enters masked (ping-pong path only: conv_nt_takes_rmask)
 };
 
 struct WgradArgs {
@@ -67,9 +64,6 @@ bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a);
 hipError_t launch_conv_nt_v2(int dtype, const ConvArgs& a, hipStream_t s);
 // ping-pong 256x256 main loop (conv_pp.hip) for the v2 cases with Co > 128
 bool conv_nt_pp_ok(const ConvArgs& a);
-// true when launch_conv_nt(dtype, 0, a) runs the ping-pong kernel, which applies a.rmask
-bool conv_nt_takes_rmask(int dtype, const ConvArgs& a);
-bool conv_nt_pp_enabled();
 hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s);
 // ping-pong 256x256 weight gradient (conv_pp.hip), used when the v2 tile choice is 256 x 256
 bool conv_wgrad_pp_ok(const WgradArgs& a);

@@ -142,10 +142,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       a_h0[j] = ok ? ho * a.sf - a.pad_h : -(1 << 28);
       a_w0[j] = wo * a.sf - a.pad_w;
       a_voff[j] = (((int)a_nb[j] + a_h0[j]) * a.W + a_w0[j]) * a.ldx * 2 + a_lc[j] * 16;
-#ifdef PP_DBG_AROWS
-      // A/B only: every tile reads the A rows of tile 0 (L2-resident source, same LDS image shape)
-      a_voff[j] = ((int)((row % PP_DBG_AROWS) * a.ldx) + a_lc[j] * 8) * 2;
-#endif
       int bits = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -444,9 +440,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     const E* R1 = (const E*)a.r;
     const E* R2 = (const E*)a.r2;
     // (persistent launches carry no residuals: pp_launch_st routes those to PERSIST = 0, whose
-    // register budget has room for the residual loads)
-    // (PERSIST == 2: persistent with residuals, A/B: the residual loads spill 3 registers)
-    const int nres = PERSIST == 1 ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
+    // register budget has room for the residual loads; a persistent variant with residuals
+    // spilled 3 registers and was no faster)
+    const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
     auto add4 = [](f32x4_t& v, const uint2 u) {
       const uint32_t w[2] = {u.x, u.y};
 #pragma unroll
@@ -464,7 +460,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
         uint2 r1v[4][2], r2v[4][2];
-        uint32_t mkv[4][2];
         if (nres) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -476,8 +471,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
               const int nc = n < a.Co ? n : 0;
               r1v[i][j] = *(const uint2*)(R1 + (size_t)mc * a.ldr + nc);
               if (nres == 2) r2v[i][j] = *(const uint2*)(R2 + (size_t)mc * a.ldr2 + nc);
-              if (a.rmask)   // the 4 ReLU bits of these channels: a nibble of the mask byte
-                mkv[i][j] = a.rmask[(size_t)mc * a.ldm + (nc >> 3)] >> (nc & 4);
             }
         }
 #pragma unroll
@@ -487,17 +480,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             const int row = wm * 128 + qm * 64 + i * 16 + lr;
             const int ch = wn * 4 + j * 2 + (lq >> 1);
             f32x4_t v = acc[qm][qn][i][j];
-            if (nres) {
-              if (a.rmask) {   // r1 = the gradient above a ReLU: masked here (no dyhat tensor)
-                const uint32_t mk = mkv[i][j];
-                uint2 u = r1v[i][j];
-                u.x &= ((mk & 1u) ? 0x0000ffffu : 0u) | ((mk & 2u) ? 0xffff0000u : 0u);
-                u.y &= ((mk & 4u) ? 0x0000ffffu : 0u) | ((mk & 8u) ? 0xffff0000u : 0u);
-                add4(v, u);
-              } else {
-                add4(v, r1v[i][j]);
-              }
-            }
+            if (nres) add4(v, r1v[i][j]);
             if (nres == 2) add4(v, r2v[i][j]);
             *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) = pack4(v);
           }
@@ -515,9 +498,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const long m = m0 + k * 32 + s_row;
-#ifdef PP_DBG_NOSTORE
-        if (v[k][0] == 0x12345678u)
-#endif
         if (m < M && n < a.Co) __builtin_nontemporal_store(v[k], (u32x4_t*)(Y + (size_t)m * a.ldy + n));
       }
       if (qn == 0) {   // the second half overwrites the staging area
@@ -543,7 +523,7 @@ __global__ __launch_bounds__(PP_THREADS, 1) void conv_nt_pp_kernel(ConvArgs a) {
   conv_nt_pp_body<E, ST, PERSIST>(a);
 }
 
-int pp_grid(int nwg, int cap = 0) {
+int pp_grid(int nwg) {
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -551,11 +531,7 @@ int pp_grid(int nwg, int cap = 0) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     ncu = (ncu + 7) / 8 * 8;   // a multiple of the XCD count keeps tile t on XCD t % 8
   }
-  const char* e = getenv("SEG_NT_PERSIST");
-  if (e && e[0] == '0') return nwg;   // one tile per workgroup (A/B)
-  int g = ncu;
-  if (cap > 0 && cap < g) g = (cap + 7) / 8 * 8;   // keep a multiple of the XCD count
-  return nwg < g ? nwg : g;
+  return nwg < ncu ? nwg : ncu;
 }
 
 template <typename E, int ST, int PERSIST>
@@ -570,24 +546,17 @@ hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
   }
   const long M = (long)a.N * a.Ho * a.Wo;
   const int nwg = ceil_div(M, 256) * ceil_div(a.Co, 256);
-  hipLaunchKernelGGL(kern, dim3(PERSIST ? pp_grid(nwg, a.grid_cap) : nwg), dim3(PP_THREADS), LDS, s, a);
+  hipLaunchKernelGGL(kern, dim3(PERSIST ? pp_grid(nwg) : nwg), dim3(PP_THREADS), LDS, s, a);
   return hipGetLastError();
 }
 
 template <typename E, int ST>
 hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
-  static const bool pres = getenv("SEG_NT_PERSIST_RES") && atoi(getenv("SEG_NT_PERSIST_RES"));
-  if ((a.r || a.r2) && pres) return pp_launch<E, ST, 2>(a, s);
   if (a.r || a.r2) return pp_launch<E, ST, 0>(a, s);
   return pp_launch<E, ST, 1>(a, s);
 }
 
 }  // namespace
-
-bool conv_nt_takes_rmask(int dtype, const ConvArgs& a) {
-  return seg_half(dtype) && a.Co > 128 && conv_nt_uses_v2(dtype, 0, a) && conv_nt_pp_enabled() &&
-         conv_nt_pp_ok(a);
-}
 
 // ping-pong config: the v2 fast-path preconditions (conv_nt_v2_ok, no tap8), Co > 128 and an
 // operands of < 2^31 bytes (32-bit buffer offsets), kernels up to 4 x 4 (tap validity bits)
@@ -805,9 +774,6 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
   auto mfma_q = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm fragment reads
     __builtin_amdgcn_sched_barrier(0);
-#ifdef PP_WG_DYNPRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -815,9 +781,6 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfq[qn][j][s], acc[qm][qn][i][j]);
-#ifdef PP_WG_DYNPRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
   };
   auto wait_next = [&](bool more) {
     if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -833,11 +796,9 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     pp_barrier();
     if (wm == 1) pp_barrier();
-#ifndef PP_WG_DYNPRIO
-    // static priority for the second-dispatched wave row (waves 4-7, the arbitration loser),
-    // no per-segment flips: wgrad 1x1 layers -2..5 % (per-segment flips: PP_WG_DYNPRIO)
+    // static priority for the second-dispatched wave row (waves 4-7, the arbitration loser);
+    // per-segment priority flips measured 2-5 % slower on the wgrad 1x1 layers
     if (wm == 1) __builtin_amdgcn_s_setprio(1);
-#endif
     for (int kb = 0; kb < nk; ++kb) {
       const bool more = kb + 1 < nk;
       if (more) decode_next();   // K-tile kb + 1

@@ -17,9 +17,7 @@
 #include <algorithm>
 #include <cstdlib>
 
-#ifndef SEG_MFMA_PRIO
-#define SEG_MFMA_PRIO 1   // s_setprio(1) around MFMA clusters (+1-2 % measured)
-#endif
+// s_setprio(1) around the MFMA clusters: +1-2 % measured
 
 // 16-byte zero source for out-of-bounds (padding) taps of the LDS-DMA gather
 __device__ __attribute__((aligned(64))) bf16_t g_zero16[64];
@@ -217,17 +215,13 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
         const int row = wn * WN + j * 16 + lr;
         bfr[j] = *(const V*)(B + row * 128 + swz(row, lq + 4 * s) * 16);
       }
-#if SEG_MFMA_PRIO
       __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = Half<E>::mma(af[i], bfr[j], acc[i][j]);
-#if SEG_MFMA_PRIO
       __builtin_amdgcn_s_setprio(0);
-#endif
     }
   };
 
@@ -443,16 +437,6 @@ hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
 
 }  // namespace
 
-// SEG_NT_PP=0 selects the v2 main loop for Co > 128 (A/B switch); default: ping-pong
-bool conv_nt_pp_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("SEG_NT_PP");
-    on = e && e[0] == '0' ? 0 : 1;
-  }
-  return on != 0;
-}
-
 // bf16 fast path: C % 64 == 0, ld/co multiples of 8; stats tiles are 256 rows
 bool conv_nt_v2_ok(const ConvArgs& a) {
   if (a.tap8)   // padded stem: 8-channel taps, weights [Co][ldw >= ceil(KH*KW*8/64)*64]
@@ -467,14 +451,14 @@ bool conv_nt_v2_ok(const ConvArgs& a) {
 // reductions K <= 512 -- 10-20 % slower than 256-row tiles on the C2 1x1 layers.)
 int conv_nt_v2_rows(const ConvArgs& a) {
   // the ping-pong kernel writes one partial per wave row (128 rows), the v2 kernels per tile
-  if (a.Co > 128 && !a.r && !a.r2 && conv_nt_pp_enabled() && conv_nt_pp_ok(a)) return 128;
+  if (a.Co > 128 && !a.r && !a.r2 && conv_nt_pp_ok(a)) return 128;
   return 256;
 }
 
 template <typename E, int ST>
 hipError_t v2_dispatch(int dtype, const ConvArgs& a, hipStream_t s) {
   if (a.Co > 128) {
-    if (conv_nt_pp_enabled() && conv_nt_pp_ok(a)) return launch_conv_nt_pp(dtype, a, s);
+    if (conv_nt_pp_ok(a)) return launch_conv_nt_pp(dtype, a, s);
     return v2_launch<E, 256, 4, 2, 2, ST>(a, s);
   }
   if (a.Co > 64) return v2_launch<E, 128, 4, 2, 3, ST>(a, s);
@@ -627,10 +611,6 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   auto tr_read = [&](const char* base, int rowb, int row, int col) -> s16x4_t {
     const int lc = col >> 3, within = (col & 7) * 2;
     const int ph = rowb >= 256 ? lc ^ (2 * (row & 3) + 8 * ((row >> 3) & 1)) : lc ^ (2 * (row & 3));
-#ifdef WG2_TR_BUILTIN
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (s16x4_t __attribute__((address_space(3)))*)(base + row * rowb + ph * 16 + within));
-#else
     // inline asm: the builtin makes hipcc wait vmcnt(0) (every LDS-DMA in flight) before the
     // read, which defeats the STAGES-deep ring; ordering is by the counted vmcnt + barrier, and
     // compute() waits lgkmcnt(0) before the MFMAs
@@ -639,7 +619,6 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
     s16x4_t r;
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
     return r;
-#endif
   };
 
   auto compute = [&](int stg) {
@@ -663,21 +642,15 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
         short t8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         __builtin_memcpy(&bfr[j], t8, 16);
       }
-#ifndef WG2_TR_BUILTIN
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-#endif
-#if SEG_MFMA_PRIO
       __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = Half<E>::mma(af[i], bfr[j], acc[i][j]);
-#if SEG_MFMA_PRIO
       __builtin_amdgcn_s_setprio(0);
-#endif
     }
   };
 
@@ -782,7 +755,7 @@ hipError_t wgrad_v2_tile_e(int dtype, const WgradArgs& a, int bm, int bn, hipStr
   }
   if (bn == 64) return wg2_launch<E, 256, 64, 8, 1, 3>(a, s);
   if (bn == 128) return wg2_launch<E, 256, 128, 4, 2, 3>(a, s);
-  if (conv_nt_pp_enabled() && conv_wgrad_pp_ok(a)) return launch_conv_wgrad_pp(dtype, a, s);
+  if (conv_wgrad_pp_ok(a)) return launch_conv_wgrad_pp(dtype, a, s);
   return wg2_launch<E, 256, 256, 2, 4, 2>(a, s);
 }
 

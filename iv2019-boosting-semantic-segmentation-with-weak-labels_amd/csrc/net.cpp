@@ -76,7 +76,9 @@ struct Unit {
 struct Prof {
   bool on = false;
   std::vector<hipEvent_t> ev;
-  struct Rec { int cls; int layer; double gflop; int e0, e1; };
+  // gflop: algorithmic work (conv classes) or algorithmic GB (BN classes); gbytes: the
+  // launch's compulsory HBM bytes (every operand read / written once) in GB
+  struct Rec { int cls; int layer; double gflop; int e0, e1; double gbytes; };
   std::vector<Rec> recs;
   int next = 0;
 };
@@ -375,7 +377,7 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
 // concurrent = the weight gradient runs on the side stream beside the dgrad -> BN chain:
 // target ~128 workgroups (half the CUs, the chain keeps the other half: 90.4 -> 92.9 img/s
 // on C2 against 512, and half the split-K slab traffic); alone (profiled, single stream,
-// seg_op_*): ~2 waves of the 256 CUs. SEG_WGRAD_WGS overrides the concurrent target.
+// seg_op_*): ~2 waves of the 256 CUs.
 int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false) {
   if (!ci) ci = L.ci;   // 8 for the tap8 stem
   int BM = L.co_pad <= 64 ? 64 : 128;
@@ -384,8 +386,7 @@ int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false) {
   if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, L.k * L.k * ci, P, &BM, &BN);
   long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * ci + BN - 1) / BN);
   // each split >= 32 K-steps of 64 pixels
-  static const long conc = getenv("SEG_WGRAD_WGS") ? atol(getenv("SEG_WGRAD_WGS")) : 128;
-  const long target = concurrent ? conc : 512;
+  const long target = concurrent ? 128 : 512;
   long s = std::max<long>(1, target / std::max<long>(tiles, 1));
   long maxs = std::max<long>(1, P / 2048);
   s = std::min(s, maxs);
@@ -401,13 +402,14 @@ struct Step {
   int dt;
 };
 
-int prof_begin(seg_ctx* c, hipStream_t s, int cls, int layer, double gflop, int* slot) {
+int prof_begin(seg_ctx* c, hipStream_t s, int cls, int layer, double gflop, int* slot,
+               double gbytes = -1.0) {
   *slot = -1;
   if (!c->prof.on) return 0;
   if (c->prof.next + 2 > (int)c->prof.ev.size()) return 0;
   int e0 = c->prof.next++, e1 = c->prof.next++;
   HIPCALL(c, hipEventRecord(c->prof.ev[e0], s));
-  c->prof.recs.push_back({cls, layer, gflop, e0, e1});
+  c->prof.recs.push_back({cls, layer, gflop, e0, e1, gbytes < 0 ? gflop : gbytes});
   *slot = (int)c->prof.recs.size() - 1;
   return 0;
 }
@@ -439,7 +441,10 @@ int conv_forward(Step& S, int li, const Act& x) {
   }
   long M = (long)x.N * L.Ho * L.Wo;
   int slot;
-  if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
+  const double esz = c->esz;   // x + w + y, each once
+  const double gbx = ((double)x.N * x.H * x.W * L.ci + (double)L.co * L.k * L.k * L.ci +
+                      (double)M * L.co) * esz * 1e-9;
+  if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot, gbx)) return r;
   HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
   if (c->bn_infer) return 0;   // is_training=False: the statistics were set for every layer
@@ -527,16 +532,19 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
 // dx = dgrad(dy) [+ r1] [+ r2]
 ConvArgs dgrad_args(seg_ctx* c, int li, const Act& dx, const Act* r1, const Act* r2);
 
-// dx = dgrad(dy) [+ r1 (ReLU-masked by r1mask when given)] [+ r2]
-int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr,
-               const uint8_t* r1mask = nullptr) {
+// dx = dgrad(dy) [+ r1] [+ r2]
+int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
   ConvArgs a = dgrad_args(c, li, dx, r1, r2);
-  if (r1mask) { a.rmask = r1mask; a.ldm = r1->C / 8; }
   long M = (long)L.N * L.H * L.W;
   int slot;
-  if (int r = prof_begin(c, S.s, 1, li, 2.0 * M * L.ci * L.k * L.k * L.co * 1e-9 / L.stride / L.stride, &slot)) return r;
+  // dy + w + dx (+ each residual read once)
+  const double nres = (r1 ? 1.0 : 0.0) + (r2 ? 1.0 : 0.0);
+  const double gbx = ((double)L.N * L.Ho * L.Wo * L.co + (double)L.co * L.k * L.k * L.ci +
+                      (double)M * L.ci * (1.0 + nres)) * c->esz * 1e-9;
+  if (int r = prof_begin(c, S.s, 1, li, 2.0 * M * L.ci * L.k * L.k * L.co * 1e-9 / L.stride / L.stride,
+                         &slot, gbx)) return r;
   HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   return prof_end(c, S.s, slot);
 }
@@ -554,9 +562,6 @@ ConvArgs dgrad_args(seg_ctx* c, int li, const Act& dx, const Act* r1, const Act*
   a.sf = 1; a.st = L.stride;
   a.pad_h = (keff - 1) - L.pad_h; a.pad_w = (keff - 1) - L.pad_w;
   a.dil = L.rate; a.stats = nullptr;
-  // beside a side-stream weight gradient the persistent dgrad takes the CUs that are free
-  static const int dgcap = getenv("SEG_DGRAD_GRID") ? atoi(getenv("SEG_DGRAD_GRID")) : 0;
-  if (c->side_active) a.grid_cap = dgcap;
   return a;
 }
 
@@ -606,7 +611,10 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   a.out = c->slab;
   long P = (long)L.N * L.Ho * L.Wo;
   int slot;
-  if (int r = prof_begin(c, S.s, 2, li, 2.0 * P * L.co * L.k * L.k * L.ci * 1e-9, &slot)) return r;
+  // dy + x (16-bit) + the fp32 weight gradient; split-K slab traffic is overhead, not algorithmic
+  const double gbx = (((double)P * L.co + (double)x.N * x.H * x.W * L.ci) * c->esz +
+                      (double)L.co * L.k * L.k * L.ci * 4.0) * 1e-9;
+  if (int r = prof_begin(c, S.s, 2, li, 2.0 * P * L.co * L.k * L.k * L.ci * 1e-9, &slot, gbx)) return r;
   HIPCALL(c, launch_conv_wgrad(S.dt, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
   if (s8) {
@@ -937,19 +945,10 @@ int unit_forward(Step& S, Unit& u) {
 
 int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
   seg_ctx* c = S.c;
-  // identity shortcut, opt-in (SEG_MASK_FOLD=1): conv1's ping-pong dgrad epilogue adds the
-  // ReLU-masked dout itself (mask bits of the unit output) so the c3 BN backward need not
-  // write the masked copy dpre. Measured 1.8 % SLOWER per step than writing dpre: the
-  // per-fragment mask-byte loads in the epilogue cost more than the saved tensor pass.
-  static const bool fold_on = getenv("SEG_MASK_FOLD") && atoi(getenv("SEG_MASK_FOLD"));
-  bool fold = false;
-  if (fold_on && u.kind == SC_IDENTITY && u.out.mask) {
-    ConvArgs t = dgrad_args(c, u.c1, dx, &u.dout, accumulate ? &dx : nullptr);
-    t.rmask = u.out.mask;
-    t.ldm = u.dout.C / 8;
-    fold = u.dout.C % 8 == 0 && conv_nt_takes_rmask(S.dt, t);
-  }
-  const Act* dpre = (u.kind != SC_CONV && !fold) ? &u.dpre : nullptr;
+  // identity / subsample shortcuts: the c3 BN backward also writes the ReLU-masked dout
+  // (dpre), the residual of the unit's input gradient. (Measured and rejected: folding the
+  // mask into conv1's dgrad epilogue instead, 1.8 % slower per step.)
+  const Act* dpre = u.kind != SC_CONV ? &u.dpre : nullptr;
   if (int r = bn_backward(S, u.c3, u.dout, 0, &u.out, dpre)) return r;
   if (u.kind == SC_CONV)
     if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
@@ -962,7 +961,6 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
   if (int r = conv_wgrad(S, u.c1, u.in)) return r;
   switch (u.kind) {
     case SC_IDENTITY:
-      if (fold) return conv_dgrad(S, u.c1, dx, &u.dout, accumulate ? &dx : nullptr, u.out.mask);
       if (accumulate) return conv_dgrad(S, u.c1, dx, &dx, &u.dpre);
       return conv_dgrad(S, u.c1, dx, &u.dpre);
     case SC_SUBSAMPLE: {
@@ -1586,8 +1584,8 @@ int seg_profile_dump(seg_ctx* c, char* buf, int len) {
     float ms = 0;
     HIPCALL(c, hipEventElapsedTime(&ms, c->prof.ev[r.e0], c->prof.ev[r.e1]));
     const ConvL& L = c->convs[r.layer];
-    snprintf(line, sizeof(line), "%d %s %d %d %d %d %d %d %.6f %.6f\n", r.cls, L.name.c_str(), L.ci,
-             L.co, L.k, L.rate, L.Ho, L.Wo, r.gflop, (double)ms);
+    snprintf(line, sizeof(line), "%d %s %d %d %d %d %d %d %.6f %.6f %.6f\n", r.cls, L.name.c_str(),
+             L.ci, L.co, L.k, L.rate, L.Ho, L.Wo, r.gflop, (double)ms, r.gbytes);
     out += line;
   }
   snprintf(buf, len, "%s", out.c_str());

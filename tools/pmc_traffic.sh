@@ -6,5 +6,5 @@ set -e
 out=$1
 mkdir -p "$out"
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $out/fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile > $out/fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $out/write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile > $out/write.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $out/fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-eval > $out/fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $out/write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-eval > $out/write.log 2>&1
