@@ -54,6 +54,8 @@ CLS_NAMES = {0: "conv_nt_pp/v2_kernel (forward implicit GEMM)",
              2: "conv_wgrad_pp/v2_kernel (weight-gradient, split-K)",
              3: "bn_apply8_kernel (BN + ReLU + residual)", 4: "bn_bwd_reduce8_kernel",
              5: "bn_bwd_apply8_kernel"}
+CLS_NAMES_F32 = {0: "conv_nt_kernel (fp32 MFMA forward)", 1: "conv_nt_kernel (fp32 MFMA data-gradient)",
+                 2: "conv_wgrad_kernel (fp32 MFMA weight-gradient, split-K)"}
 EMA_DECAY = 0.9   # utils/utils.py:112 default; off when distributed (system_factory.py:236-238)
 
 
@@ -254,12 +256,13 @@ def main():
             gf = sum(v[0] for v in dil.values()); ms_ = sum(v[1] for v in dil.values())
             dilated["all"] = {"achieved": round(gf / ms_, 1), "frac": round(gf / ms_ / peak, 4),
                               "unit": "TFLOP/s"}
+        names = dict(CLS_NAMES, **(CLS_NAMES_F32 if args.dtype == "fp32" else {}))
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                     "traffic_source": tsrc,
                     "algorithmic_bytes": round(alg_bytes),
                     "traffic_ratio": round(traffic / alg_bytes, 3) if traffic and alg_bytes else None,
-                    "kernel": CLS_NAMES[dom],
+                    "kernel": names[dom],
                     "launches": r["launches"],
                     "avg_launch_ms": round(r["ms"] / max(r["launches"], 1), 4),
                     # fwd + dgrad share the conv_nt*_kernel names in a rocprofv3 trace: their

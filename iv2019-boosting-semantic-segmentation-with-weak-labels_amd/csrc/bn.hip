@@ -8,47 +8,82 @@
 
 namespace {
 
-// ---- forward statistics: one-launch finalize (a two-launch Chan merge measured slower): per-tile (sum, M2)
-// partials of tile_rows rows (the last one ragged) merged as shifted sums around tile 0's mean
-// p: A = sum_t n_t (mean_t - p), B = sum_t (M2_t + n_t (mean_t - p)^2), so mean = p + A / N and
-// var = B / N - (A / N)^2, with no division per merge; 8 channels x 64 tile lanes per block,
-// fixed summation order (bitwise reproducible)
-constexpr int SF_CH = 8, SF_LANES = 64;
-constexpr int BF_CH = 8, BF_LANES = 64;   // backward finalize: more blocks, shorter loops
-__global__ __launch_bounds__(SF_CH * SF_LANES) void bn_stats_final_kernel(
+// ---- forward statistics: one-launch finalize (a two-launch Chan merge measured slower) ----
+// per-tile (sum, M2) partials of tile_rows rows (the last one ragged) merged as shifted sums
+// around tile 0's mean p: A = sum_t n_t (mean_t - p), B = sum_t (M2_t + n_t (mean_t - p)^2), so
+// mean = p + A / N and var = B / N - (A / N)^2, with no division per merge. Block = 8 channels
+// x 256 tile lanes (4 waves): every lane keeps FIN_U tiles x 8 channels of loads in flight,
+// then a fixed xor butterfly inside each wave and a fixed-order sum of the 4 wave results
+// (bitwise reproducible). The previous layout (64 tile lanes, a 63-step serial LDS sum on one
+// thread) took ~11 us per layer, mostly latency.
+constexpr int FIN_CH = 8, FIN_THREADS = 256, FIN_U = 4;
+
+template <int NV>
+__device__ __forceinline__ void wave_sum_xor(float (&v)[NV]) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[e] += __shfl_xor(v[e], o, 64);
+}
+
+__global__ __launch_bounds__(FIN_THREADS) void bn_stats_final_kernel(
     const float* __restrict__ part, long M, int C, int tile_rows, int ntiles,
     const float* __restrict__ gamma, BnState st, float* pack) {
-  __shared__ float sh[2][SF_LANES][SF_CH];
-  const int cl = threadIdx.x % SF_CH, tl = threadIdx.x / SF_CH;
-  const int c = blockIdx.x * SF_CH + cl;
-  float A = 0.f, B = 0.f, p = 0.f;
-  if (c < C) {
-    const float fr = (float)tile_rows, inv_fr = 1.f / fr;
-    const float2 v0 = *(const float2*)(part + 2 * (size_t)c);
-    p = M < tile_rows ? v0.x / (float)M : v0.x * inv_fr;
-#pragma unroll 4
-    for (int t = tl; t < ntiles; t += SF_LANES) {
-      const float2 v = *(const float2*)(part + 2 * ((size_t)t * C + c));
+  __shared__ float sh[FIN_THREADS / 64][2 * FIN_CH];
+  const int c0 = blockIdx.x * FIN_CH;
+  const int nch = C - c0 < FIN_CH ? C - c0 : FIN_CH;
+  const float fr = (float)tile_rows, inv_fr = 1.f / fr;
+  float p[FIN_CH], ab[2 * FIN_CH];
+#pragma unroll
+  for (int e = 0; e < FIN_CH; ++e) {
+    const float s0 = e < nch ? part[2 * (size_t)(c0 + e)] : 0.f;
+    p[e] = M < tile_rows ? s0 / (float)M : s0 * inv_fr;
+    ab[e] = 0.f;
+    ab[FIN_CH + e] = 0.f;
+  }
+  for (int t0 = 0; t0 < ntiles; t0 += FIN_THREADS * FIN_U) {
+    float2 v[FIN_U][FIN_CH];
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) {
+      const int t = t0 + u * FIN_THREADS + (int)threadIdx.x;
+#pragma unroll
+      for (int e = 0; e < FIN_CH; ++e)
+        v[u][e] = (t < ntiles && e < nch) ? *(const float2*)(part + 2 * ((size_t)t * C + c0 + e))
+                                          : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) {
+      const int t = t0 + u * FIN_THREADS + (int)threadIdx.x;
+      if (t >= ntiles) continue;
       const long rows = M - (long)t * tile_rows;
       const bool rag = rows < tile_rows;
       const float n = rag ? (float)rows : fr;
-      const float d = (rag ? v.x / n : v.x * inv_fr) - p;
-      A = __builtin_fmaf(n, d, A);
-      B += __builtin_fmaf(n * d, d, v.y);
+#pragma unroll
+      for (int e = 0; e < FIN_CH; ++e) {
+        const float d = (rag ? v[u][e].x / n : v[u][e].x * inv_fr) - p[e];
+        ab[e] = __builtin_fmaf(n, d, ab[e]);
+        ab[FIN_CH + e] += __builtin_fmaf(n * d, d, v[u][e].y);
+      }
     }
   }
-  sh[0][tl][cl] = A;
-  sh[1][tl][cl] = B;
+  wave_sum_xor(ab);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int e = 0; e < 2 * FIN_CH; ++e) sh[w][e] = ab[e];
   __syncthreads();
-  if (tl == 0 && c < C) {
-#pragma unroll 8
-    for (int k = 1; k < SF_LANES; ++k) {
-      A += sh[0][k][cl];
-      B += sh[1][k][cl];
+  const int e = threadIdx.x;
+  if (e < nch) {
+    float A = sh[0][e], B = sh[0][FIN_CH + e];
+#pragma unroll
+    for (int k = 1; k < FIN_THREADS / 64; ++k) {
+      A += sh[k][e];
+      B += sh[k][FIN_CH + e];
     }
+    const int c = c0 + e;
     const float N = (float)M;
     const float dm = A / N;
-    const float mean = p + dm;
+    const float mean = p[e] + dm;
     const float var = fmaxf(B / N - dm * dm, 0.f);
     const float inv = rsqrtf(var + SEG_BN_EPS);
     st.mean[c] = mean;
@@ -62,32 +97,50 @@ __global__ __launch_bounds__(SF_CH * SF_LANES) void bn_stats_final_kernel(
   }
 }
 
-// backward finalize: sums of the per-row-block (sum dyhat, sum dyhat*xhat) partials, 32
-// channels x 64 partial lanes per block, fixed order
-__global__ __launch_bounds__(BF_CH * BF_LANES) void bn_bwd_final_kernel(
+// backward finalize: sums of the per-row-block (sum dyhat, sum dyhat*xhat) partials, the same
+// 8 channels x 256 lanes layout and fixed reduction order
+__global__ __launch_bounds__(FIN_THREADS) void bn_bwd_final_kernel(
     const float* __restrict__ part, int rb, long M, int C, BnState st, float* dgamma,
     float* dbeta) {
-  __shared__ float sh[2][BF_LANES][BF_CH];
-  const int cl = threadIdx.x % BF_CH, tl = threadIdx.x / BF_CH;
-  const int c = blockIdx.x * BF_CH + cl;
-  float s1 = 0.f, s2 = 0.f;
-  if (c < C) {
-#pragma unroll 4
-    for (int k = tl; k < rb; k += BF_LANES) {
-      const float2 v = *(const float2*)(part + 2 * ((size_t)k * C + c));
-      s1 += v.x;
-      s2 += v.y;
+  __shared__ float sh[FIN_THREADS / 64][2 * FIN_CH];
+  const int c0 = blockIdx.x * FIN_CH;
+  const int nch = C - c0 < FIN_CH ? C - c0 : FIN_CH;
+  float s[2 * FIN_CH];
+#pragma unroll
+  for (int e = 0; e < 2 * FIN_CH; ++e) s[e] = 0.f;
+  for (int k0 = 0; k0 < rb; k0 += FIN_THREADS * FIN_U) {
+    float2 v[FIN_U][FIN_CH];
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) {
+      const int k = k0 + u * FIN_THREADS + (int)threadIdx.x;
+#pragma unroll
+      for (int e = 0; e < FIN_CH; ++e)
+        v[u][e] = (k < rb && e < nch) ? *(const float2*)(part + 2 * ((size_t)k * C + c0 + e))
+                                      : make_float2(0.f, 0.f);
     }
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u)
+#pragma unroll
+      for (int e = 0; e < FIN_CH; ++e) {
+        s[e] += v[u][e].x;
+        s[FIN_CH + e] += v[u][e].y;
+      }
   }
-  sh[0][tl][cl] = s1;
-  sh[1][tl][cl] = s2;
+  wave_sum_xor(s);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int e = 0; e < 2 * FIN_CH; ++e) sh[w][e] = s[e];
   __syncthreads();
-  if (tl == 0 && c < C) {
-#pragma unroll 8
-    for (int k = 1; k < BF_LANES; ++k) {
-      s1 += sh[0][k][cl];
-      s2 += sh[1][k][cl];
+  const int e = threadIdx.x;
+  if (e < nch) {
+    float s1 = sh[0][e], s2 = sh[0][FIN_CH + e];
+#pragma unroll
+    for (int k = 1; k < FIN_THREADS / 64; ++k) {
+      s1 += sh[k][e];
+      s2 += sh[k][FIN_CH + e];
     }
+    const int c = c0 + e;
     st.sdy[c] = s1 / (float)M;
     st.sdyx[c] = s2 / (float)M;
     if (dgamma) dgamma[c] = s2;
@@ -672,7 +725,7 @@ hipError_t launch_bn_stats_finalize(const float* tile_part, long M, int C, int t
                                     hipStream_t s, float* pack) {
   int ntiles = ceil_div(M, tile_rows);
   (void)scratch;
-  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(ceil_div(C, SF_CH)), dim3(SF_CH * SF_LANES), 0,
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(ceil_div(C, FIN_CH)), dim3(FIN_THREADS), 0,
                      s, tile_part, M, C, tile_rows, ntiles, gamma, st, pack);
   return hipGetLastError();
 }
@@ -732,7 +785,7 @@ hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipSt
 
 hipError_t launch_bn_bwd_finalize(const float* part, int rb, long M, int C, BnState st,
                                   float* dgamma, float* dbeta, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ceil_div(C, BF_CH)), dim3(BF_CH * BF_LANES), 0, s,
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ceil_div(C, FIN_CH)), dim3(FIN_THREADS), 0, s,
                      part, rb, M, C, st, dgamma, dbeta);
   return hipGetLastError();
 }

@@ -62,6 +62,10 @@ int conv_nt_v2_rows(const ConvArgs& a);   // tile rows (= BN-stat partial rows) 
 // true when launch_conv_nt runs the v2 kernel
 bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a);
 hipError_t launch_conv_nt_v2(int dtype, const ConvArgs& a, hipStream_t s);
+// skinny 1x1 convs (skinny.hip): N <= 16 (the logits convs, with BN partials per 128 rows) or
+// K <= 16 (their data gradients), 16-bit storage; taken where the v2 kernels cannot run
+bool conv_skinny_ok(int dtype, int out_f32, const ConvArgs& a);
+hipError_t launch_conv_skinny(int dtype, const ConvArgs& a, hipStream_t s);
 // ping-pong 256x256 main loop (conv_pp.hip) for the v2 cases with Co > 128
 bool conv_nt_pp_ok(const ConvArgs& a);
 hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s);

@@ -722,6 +722,7 @@ bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a) {
 
 hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t s) {
   if (conv_nt_uses_v2(dtype, out_f32, a)) return launch_conv_nt_v2(dtype, a, s);
+  if (conv_skinny_ok(dtype, out_f32, a)) return launch_conv_skinny(dtype, a, s);
   if (dtype == SEG_BF16) {
     if (out_f32) return nt_dispatch<bf16_t, float>(a, s);
     return nt_dispatch<bf16_t, bf16_t>(a, s);

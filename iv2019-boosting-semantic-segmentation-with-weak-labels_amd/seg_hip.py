@@ -381,7 +381,7 @@ class SegContext:
             f = line.split()
             rows.append(dict(cls=int(f[0]), name=f[1], ci=int(f[2]), co=int(f[3]), k=int(f[4]),
                              rate=int(f[5]), ho=int(f[6]), wo=int(f[7]), gflop=float(f[8]),
-                             ms=float(f[9]), gbytes=float(f[10])))
+                             ms=float(f[9]), gbytes=float(f[10]) if len(f) > 10 else 0.0))
         return rows
 
     def close(self):

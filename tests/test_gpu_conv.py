@@ -17,7 +17,9 @@ CASES = [
     (1, 11, 9, 256, 128, 1, 1, 1, False),     # 1x1
     (2, 18, 22, 64, 64, 3, 2, 1, True),       # conv2d_same stride 2
     (1, 37, 45, 3, 64, 7, 2, 1, True),        # stem (generic small-C path)
-    (2, 9, 10, 256, 14, 1, 1, 1, False),      # logits (Co=14)
+    (2, 9, 10, 256, 14, 1, 1, 1, False),      # logits (Co=14): skinny narrow-N / narrow-K
+    (1, 37, 45, 256, 7, 1, 1, 1, False),      # l2 vehicle logits, ragged 128-row stats tiles
+    (2, 9, 10, 256, 3, 1, 1, 1, False),       # l2 human logits
     (1, 6, 6, 1280, 256, 1, 1, 1, False),     # PSP final (C=1280)
     (2, 15, 21, 256, 512, 1, 1, 1, False),    # short K, wide N: 128-row tiles, 2 per CU
 ]
@@ -76,15 +78,17 @@ def test_conv_fwd(cuda, dtype, case):
     ref = _ref_conv(x, w, spec)
     xd = torch.as_tensor(x).to(cuda, tdt).contiguous()
     wd = torch.as_tensor(w).to(cuda, tdt).contiguous()
-    yd = torch.zeros((N, Ho, Wo, Co), dtype=tdt, device=cuda)
+    # narrow outputs (the logits) live in 16-channel pixels, as the runtime lays them out
+    ldy = Co if Co % 8 == 0 else (Co + 15) // 16 * 16
+    yd = torch.zeros((N, Ho, Wo, ldy), dtype=tdt, device=cuda)
     M = N * Ho * Wo
     stats = torch.zeros(((M + 127) // 128, Co, 2), dtype=torch.float32, device=cuda)
     s_ = torch.cuda.current_stream().cuda_stream
     check(LIB.seg_op_conv_fwd(ABI[dtype], xd.data_ptr(), N, H, W, Ci, Ci,
-                              wd.data_ptr(), Co, k, s, r, int(ep), yd.data_ptr(), Co,
+                              wd.data_ptr(), Co, k, s, r, int(ep), yd.data_ptr(), ldy,
                               stats.data_ptr(), s_))
     torch.cuda.synchronize()
-    y = yd.float().cpu().numpy()
+    y = yd[..., :Co].float().cpu().numpy()
     tol = TOL[dtype]
     assert _rel(y, ref) < tol
     # BN partial statistics: merge (sum, M2 about the tile mean) and compare
@@ -120,10 +124,14 @@ def test_conv_dgrad(cuda, dtype, case):
     y.backward(torch.as_tensor(g, dtype=torch.float64).permute(0, 3, 1, 2))
     ref = xt.grad.permute(0, 2, 3, 1).numpy()
     wt = np.ascontiguousarray(np.flip(w, (1, 2)).transpose(3, 1, 2, 0))  # [Ci][k][k][Co] flipped
-    gd = torch.as_tensor(g).to(cuda, tdt).contiguous()
+    # narrow gradients (of the logits) come in 16-channel pixels, as the runtime lays them out
+    lddy = Co if Co % 8 == 0 else (Co + 15) // 16 * 16
+    gp = np.zeros(g.shape[:3] + (lddy,), np.float32)
+    gp[..., :Co] = g
+    gd = torch.as_tensor(gp).to(cuda, tdt).contiguous()
     wtd = torch.as_tensor(wt).to(cuda, tdt).contiguous()
     dx = torch.zeros((N, H, W, Ci), dtype=tdt, device=cuda)
-    check(LIB.seg_op_conv_dgrad(ABI[dtype], gd.data_ptr(), N, Ho, Wo, Co, Co,
+    check(LIB.seg_op_conv_dgrad(ABI[dtype], gd.data_ptr(), N, Ho, Wo, Co, lddy,
                                 wtd.data_ptr(), Ci, k, s, r, int(ep), H, W, dx.data_ptr(), Ci,
                                 torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()

@@ -90,6 +90,7 @@ C2_LAYERS = [
     ("aspp_conv_r18", 4, 128, 256, 256, 256, 3, 1, 18, False),
     ("block1_conv2_s2", 4, 256, 512, 64, 64, 3, 2, 1, True),
     ("block2_conv1_co128", 4, 128, 256, 256, 128, 1, 1, 1, False),
+    ("l1_logits_co14", 4, 128, 256, 256, 14, 1, 1, 1, False),
 ]
 LAYER_DTYPES = [(c, "bf16") for c in C2_LAYERS] + [(C2_LAYERS[0], "fp16"), (C2_LAYERS[2], "fp16")]
 
@@ -151,7 +152,10 @@ def test_conv_c2_layer(cuda, case, dtype):
     torch.cuda.synchronize()
     _elementwise(dx, ref.to(cuda), 2 * ULP[dtype], 1e-3, f"{name} dgrad")
     del dx, wtd
-    # ---- weight gradient (split-K over the 131 k - 524 k pixels, fp32 slabs + reduce)
+    # ---- weight gradient (split-K over the 131 k - 524 k pixels, fp32 slabs + reduce); the
+    # runtime pads Co % 8 != 0 rows (the logits) itself: that one is covered by the step test
+    if Co % 8:
+        return
     wg = torch.zeros(Co, k, k, Ci, requires_grad=True)
     conv_tf(x.float().permute(0, 3, 1, 2), wg, spec).backward(dy.float().permute(0, 3, 1, 2))
     dw = torch.zeros((Co, k, k, Ci), dtype=torch.float32, device=cuda)
