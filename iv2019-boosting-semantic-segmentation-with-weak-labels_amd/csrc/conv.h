@@ -26,8 +26,8 @@ struct ConvArgs {
   int st;         // transposed stride: src valid iff divisible by st (1 = plain conv)
   int pad_h, pad_w, dil;
   float* stats;   // BN partials [mtiles][Co] x {sum, M2} (nullptr = none)
-  int tap8;       // 1: C == 8 and every 16-B chunk of K is one tap (the 3-channel stem padded
-                  // to 8); K = KH*KW*8 is padded to a multiple of 64 with zero weights
+  int tap8;       // tap mode: a tap is tap8 16-B chunks of K (2: the space-to-depth stem, 16
+                  // channels per tap); K = KH*KW*C is padded to a multiple of 64 with zero weights
 };
 
 struct WgradArgs {
@@ -77,12 +77,18 @@ hipError_t launch_conv_wgrad_v2(int dtype, const WgradArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad_v2_tile(int dtype, const WgradArgs& a, int bm, int bn, hipStream_t s);
 void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn);
 
-// 3-channel stem in 16-bit storage, laid out as 8-channel taps (tap8 mode):
-//   images f32 [M][3] -> bf16/fp16 [M][8] (channels 3..7 zero)
-hipError_t launch_cast_pad8(int dtype, const float* src, void* dst, long M, hipStream_t s);
-//   weights bf16 [Co][taps][ci] -> [Co][ldw] with 8-channel taps, zero padded
-hipError_t launch_stem_pad_weights(const bf16_t* w, bf16_t* wp, int co, int taps, int ci, int ldw,
-                                   hipStream_t s);
-//   split-K slabs [splits][co_pad][taps*8] -> fp32 [co][taps][ci] (drops the pad channels)
-hipError_t launch_splitk_reduce_pad8(const float* part, int splits, long split_stride, int co,
-                                     int taps, int ci, float* out, hipStream_t s);
+// 7x7 / 2 stem (3 channels) in 16-bit storage as a 4x4 / 1 VALID conv over a space-to-depth
+// image: X'[n][i][j][(dh*2 + dw)*3 + c] = x[n][2i + dh - pad_h][2j + dw - pad_w][c] (channels
+// 12..15 zero), Hs = Ho + 3, Ws = Wo + 3; w'[co][a][b][(dh*2 + dw)*3 + c] = w[co][2a+dh][2b+dw][c]
+// (zero past the 7x7 kernel), K = 4 * 4 * 16 = 256 (tap mode, tap8 = 2)
+//   images f32 [N][H][W][3] -> s2d [N][Hs][Ws][16]
+hipError_t launch_cast_s2d(int dtype, const float* src, void* dst, int N, int H, int W, int Hs, int Ws,
+                           int pad_h, int pad_w, hipStream_t s);
+//   s2d [N][Hs][Ws][16] -> [N][H][W][8] (channels 0..2 the image, 3..7 zero): parity tests' view
+hipError_t launch_unshuffle_s2d(const void* src, void* dst, int N, int H, int W, int Hs, int Ws,
+                                int pad_h, int pad_w, hipStream_t s);
+//   weights 16-bit [Co][7][7][3] -> [Co][256]
+hipError_t launch_stem_s2d_weights(const bf16_t* w, bf16_t* wp, int co, hipStream_t s);
+//   split-K slabs [splits][co_pad][256] of the s2d weight gradient -> fp32 [co][7][7][3]
+hipError_t launch_splitk_reduce_s2d(const float* part, int splits, long split_stride, int co,
+                                    float* out, hipStream_t s);

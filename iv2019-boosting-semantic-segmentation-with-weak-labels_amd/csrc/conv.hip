@@ -646,73 +646,128 @@ __device__ __forceinline__ uint32_t bits16(float v) {
   __builtin_memcpy(&b, &h, 2);
   return b;
 }
+// space-to-depth stem image: one thread per s2d pixel (i, j) of image n: the 2 x 2 source
+// block (rows 2i + dh - pad_h, columns 2j + dw - pad_w), 3 channels each, as 12 16-bit values
+// plus 4 zeros, two 16-B stores
 template <typename E>
-__global__ void cast_pad8_kernel(const float* __restrict__ src, E* __restrict__ dst, long M) {
-  for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (long)gridDim.x * blockDim.x) {
-    const float* p = src + 3 * m;
-    const uint32_t w0 = bits16<E>(p[0]) | (bits16<E>(p[1]) << 16);
-    const uint32_t w1 = bits16<E>(p[2]);
-    *(uint4*)(dst + 8 * m) = make_uint4(w0, w1, 0u, 0u);
+__global__ void cast_s2d_kernel(const float* __restrict__ src, E* __restrict__ dst, int N, int H,
+                                int W, int Hs, int Ws, int ph, int pw) {
+  const long total = (long)N * Hs * Ws;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(q % Ws);
+    const long t = q / Ws;
+    const int i = (int)(t % Hs), n = (int)(t / Hs);
+    uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int h = 2 * i + dh - ph, x = 2 * j + dw - pw;
+        const bool ok = (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W;
+        const float* p = src + (((size_t)n * H + (ok ? h : 0)) * W + (ok ? x : 0)) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const int ch = (dh * 2 + dw) * 3 + c;
+          w[ch >> 1] |= (ok ? bits16<E>(p[c]) : 0u) << ((ch & 1) * 16);
+        }
+      }
+    E* o = dst + (size_t)q * 16;
+    *(uint4*)o = make_uint4(w[0], w[1], w[2], w[3]);
+    *(uint4*)(o + 8) = make_uint4(w[4], w[5], w[6], w[7]);
   }
 }
-__global__ void stem_pad_weights_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp,
-                                        int co, int taps, int ci, int ldw) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= co * ldw) return;
-  const int o = i / ldw, k = i - o * ldw;
-  const int t = k >> 3, c = k & 7;
-  wp[i] = (t < taps && c < ci) ? w[((size_t)o * taps + t) * ci + c] : (bf16_t)0;
+// inverse view for the parity tests: [N][H][W][8], channels 0..2 = the 16-bit image
+__global__ void unshuffle_s2d_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                     int N, int H, int W, int Hs, int Ws, int ph, int pw) {
+  const long total = (long)N * H * W;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(q % W);
+    const long t = q / W;
+    const int h = (int)(t % H), n = (int)(t / H);
+    const int hh = h + ph, xx = x + pw;
+    const uint16_t* p = src + (((size_t)n * Hs + (hh >> 1)) * Ws + (xx >> 1)) * 16 + ((hh & 1) * 2 + (xx & 1)) * 3;
+    uint16_t* o = dst + (size_t)q * 8;
+    o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+#pragma unroll
+    for (int c = 3; c < 8; ++c) o[c] = 0;
+  }
 }
-// stem weight gradient: few outputs (co * 49 * 3) over many splits, so 8 lanes per output
-// each sum every 8th split, then a fixed-order tree over the lanes (one serial loop per
-// output over 256 splits took 82 us)
-constexpr int RP8_OUT = 32, RP8_LANES = 8;
-__global__ __launch_bounds__(RP8_OUT * RP8_LANES) void splitk_reduce_pad8_kernel(
-    const float* __restrict__ part, int splits, long stride, int co, int taps, int ci,
-    float* __restrict__ out) {
-  __shared__ float sh[RP8_LANES][RP8_OUT];
-  const int ol = threadIdx.x % RP8_OUT, zl = threadIdx.x / RP8_OUT;
-  const int i = blockIdx.x * RP8_OUT + ol;
-  const int n = co * taps * ci;
+// w'[co][a][b][(dh*2 + dw)*3 + c] = w[co][2a + dh][2b + dw][c] inside the 7 x 7 kernel, else 0
+__global__ void stem_s2d_weights_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp, int co) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= co * 256) return;
+  const int o = i >> 8, k = i & 255;
+  const int tap = k >> 4, ch = k & 15;
+  const int a = tap >> 2, b = tap & 3;
+  bf16_t v = 0;
+  if (ch < 12) {
+    const int q = ch / 3, c = ch - q * 3;
+    const int kh = 2 * a + (q >> 1), kw = 2 * b + (q & 1);
+    if (kh < 7 && kw < 7) v = w[((o * 7 + kh) * 7 + kw) * 3 + c];
+  }
+  wp[i] = v;
+}
+// stem weight gradient: few outputs (co * 147) over many splits, so 8 lanes per output each sum
+// every 8th split, then a fixed-order sum over the lanes; output (o, kh, kw, c) reads the s2d
+// column ((kh/2)*4 + kw/2)*16 + ((kh%2)*2 + kw%2)*3 + c
+constexpr int RS_OUT = 32, RS_LANES = 8;
+__global__ __launch_bounds__(RS_OUT * RS_LANES) void splitk_reduce_s2d_kernel(
+    const float* __restrict__ part, int splits, long stride, int co, float* __restrict__ out) {
+  __shared__ float sh[RS_LANES][RS_OUT];
+  const int ol = threadIdx.x % RS_OUT, zl = threadIdx.x / RS_OUT;
+  const int i = blockIdx.x * RS_OUT + ol;
+  const int n = co * 147;
   float acc = 0.f;
   if (i < n) {
-    const int o = i / (taps * ci), r = i - o * taps * ci;
-    const int t = r / ci, c = r - t * ci;
-    const long src = (long)o * taps * 8 + t * 8 + c;
+    const int o = i / 147, r = i - o * 147;
+    const int kh = r / 21, kw = (r - kh * 21) / 3, c = r - kh * 21 - kw * 3;
+    const long src = (long)o * 256 + ((kh >> 1) * 4 + (kw >> 1)) * 16 + ((kh & 1) * 2 + (kw & 1)) * 3 + c;
 #pragma unroll 4
-    for (int z = zl; z < splits; z += RP8_LANES) acc += part[(size_t)z * stride + src];
+    for (int z = zl; z < splits; z += RS_LANES) acc += part[(size_t)z * stride + src];
   }
   sh[zl][ol] = acc;
   __syncthreads();
   if (zl == 0 && i < n) {
     float v = sh[0][ol];
 #pragma unroll
-    for (int k = 1; k < RP8_LANES; ++k) v += sh[k][ol];
+    for (int k = 1; k < RS_LANES; ++k) v += sh[k][ol];
     out[i] = v;
   }
 }
 }  // namespace
 
-hipError_t launch_cast_pad8(int dtype, const float* src, void* dst, long M, hipStream_t s) {
-  long g = (M + 255) / 256;
+static dim3 grid_of(long items) {
+  long g = (items + 255) / 256;
   if (g > 8192) g = 8192;
-  const dim3 grid((int)(g < 1 ? 1 : g));
+  return dim3((unsigned)(g < 1 ? 1 : g));
+}
+
+hipError_t launch_cast_s2d(int dtype, const float* src, void* dst, int N, int H, int W, int Hs, int Ws,
+                           int pad_h, int pad_w, hipStream_t s) {
+  const dim3 g = grid_of((long)N * Hs * Ws);
   if (dtype == SEG_F16)
-    hipLaunchKernelGGL(cast_pad8_kernel<f16_t>, grid, dim3(256), 0, s, src, (f16_t*)dst, M);
+    hipLaunchKernelGGL(cast_s2d_kernel<f16_t>, g, dim3(256), 0, s, src, (f16_t*)dst, N, H, W, Hs, Ws,
+                       pad_h, pad_w);
   else
-    hipLaunchKernelGGL(cast_pad8_kernel<bf16_t>, grid, dim3(256), 0, s, src, (bf16_t*)dst, M);
+    hipLaunchKernelGGL(cast_s2d_kernel<bf16_t>, g, dim3(256), 0, s, src, (bf16_t*)dst, N, H, W, Hs, Ws,
+                       pad_h, pad_w);
   return hipGetLastError();
 }
-hipError_t launch_stem_pad_weights(const bf16_t* w, bf16_t* wp, int co, int taps, int ci, int ldw,
-                                   hipStream_t s) {
-  hipLaunchKernelGGL(stem_pad_weights_kernel, dim3(ceil_div((long)co * ldw, 256)), dim3(256), 0, s, w,
-                     wp, co, taps, ci, ldw);
+hipError_t launch_unshuffle_s2d(const void* src, void* dst, int N, int H, int W, int Hs, int Ws,
+                                int pad_h, int pad_w, hipStream_t s) {
+  hipLaunchKernelGGL(unshuffle_s2d_kernel, grid_of((long)N * H * W), dim3(256), 0, s,
+                     (const uint16_t*)src, (uint16_t*)dst, N, H, W, Hs, Ws, pad_h, pad_w);
   return hipGetLastError();
 }
-hipError_t launch_splitk_reduce_pad8(const float* part, int splits, long split_stride, int co,
-                                     int taps, int ci, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(splitk_reduce_pad8_kernel, dim3(ceil_div((long)co * taps * ci, RP8_OUT)),
-                     dim3(RP8_OUT * RP8_LANES), 0, s, part, splits, split_stride, co, taps, ci, out);
+hipError_t launch_stem_s2d_weights(const bf16_t* w, bf16_t* wp, int co, hipStream_t s) {
+  hipLaunchKernelGGL(stem_s2d_weights_kernel, dim3(ceil_div((long)co * 256, 256)), dim3(256), 0, s, w,
+                     wp, co);
+  return hipGetLastError();
+}
+hipError_t launch_splitk_reduce_s2d(const float* part, int splits, long split_stride, int co,
+                                    float* out, hipStream_t s) {
+  hipLaunchKernelGGL(splitk_reduce_s2d_kernel, dim3(ceil_div((long)co * 147, RS_OUT)),
+                     dim3(RS_OUT * RS_LANES), 0, s, part, splits, split_stride, co, out);
   return hipGetLastError();
 }
 

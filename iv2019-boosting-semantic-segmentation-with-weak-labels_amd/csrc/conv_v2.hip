@@ -104,7 +104,7 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
   const long m0 = (long)mt * BM;
   const int n0 = nt * BN;
   const int K = a.KH * a.KW * a.C;
-  const int nk = T8 ? (K + BK - 1) / BK : K / BK;   // T8: taps beyond KH*KW read zeros
+  const int nk = T8 ? (K + BK - 1) / BK : K / BK;   // tap mode: taps beyond KH*KW read zeros
   const E* X = (const E*)a.x;
   const E* Wt = (const E*)a.w;
 
@@ -143,8 +143,12 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
     for (int i = 0; i < AR; ++i) {
       const int lc = swz(a_row[i], pc);
       int hi = a_h0[i] + dh, wi = a_w0[i] + dw;
-      if constexpr (T8) {   // one tap per 16-B chunk: this lane's tap is kb*8 + lc
-        const int t8 = kb * 8 + lc;
+      int coff = 0;
+      if constexpr (T8) {   // tap mode: a tap is T8 16-B chunks (8 channels each); this lane's
+                            // chunk is kb*8 + lc, its tap (kb*8 + lc) / T8
+        const int ch = kb * 8 + lc;
+        const int t8 = ch / T8;
+        coff = (ch - t8 * T8) * 8;
         const int kh8 = t8 / a.KW, kw8 = t8 - kh8 * a.KW;
         hi = t8 < a.KH * a.KW ? a_h0[i] + kh8 * a.dil : -1;
         wi = a_w0[i] + kw8 * a.dil;
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
         wi /= ST;
         ok &= (hi < a.H) & (wi < a.W);
       }
-      const size_t off = ((size_t)(a_nb[i] + hi) * a.W + wi) * a.ldx + c0 + (T8 ? 0 : lc * 8);
+      const size_t off = ((size_t)(a_nb[i] + hi) * a.W + wi) * a.ldx + c0 + (T8 ? coff : lc * 8);
       glds16(ok ? (const void*)(X + off) : (const void*)zero, sA + (i * 8 + wave) * 1024);
     }
   };
@@ -439,9 +443,11 @@ hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
 
 // bf16 fast path: C % 64 == 0, ld/co multiples of 8; stats tiles are 256 rows
 bool conv_nt_v2_ok(const ConvArgs& a) {
-  if (a.tap8)   // padded stem: 8-channel taps, weights [Co][ldw >= ceil(KH*KW*8/64)*64]
-    return a.st == 1 && a.C == 8 && a.ldx == 8 && a.Co <= 64 && (a.Co % 8) == 0 && (a.ldy % 8) == 0 &&
-           a.ldw >= (a.KH * a.KW * 8 + BK - 1) / BK * BK && (a.ldw % 8) == 0 && !a.r && !a.r2;
+  if (a.tap8)   // tap mode (the space-to-depth stem): taps of C = 8 * tap8 channels (tap8 = 2),
+                // weights [Co][ldw >= ceil(KH*KW*C/64)*64]
+    return a.tap8 == 2 && a.st == 1 && a.C == 16 && a.ldx == 16 && a.Co <= 64 && (a.Co % 8) == 0 &&
+           (a.ldy % 8) == 0 && a.ldw >= (a.KH * a.KW * a.C + BK - 1) / BK * BK && (a.ldw % 8) == 0 &&
+           !a.r && !a.r2;
   return (a.st == 1 || a.st == 2) && (a.C % BK) == 0 && (a.ldx % 8) == 0 && (a.ldw % 8) == 0 && (a.Co % 8) == 0 &&
          (a.ldy % 8) == 0 && (!a.r || a.ldr % 8 == 0) && (!a.r2 || a.ldr2 % 8 == 0);
 }
@@ -449,10 +455,15 @@ bool conv_nt_v2_ok(const ConvArgs& a) {
 // rows per tile of the v2 config launch_conv_nt_v2 picks (= BN-statistics partial rows).
 // (Measured and rejected: 128 x 128 tiles with a 64 KB ring, two workgroups per CU, for short
 // reductions K <= 512 -- 10-20 % slower than 256-row tiles on the C2 1x1 layers.)
+// 128-row tiles, two workgroups per CU, for the narrow (Co <= 64) layers -- the stem and block1:
+// short reductions whose one-tile-per-CU 256-row launches were latency-bound (stem forward
+// 287 -> 241 us, block1 1x1 / 3x3 layers 4-18 % faster)
+static bool v2_small_tile(const ConvArgs& a) { return a.Co <= 64; }
+
 int conv_nt_v2_rows(const ConvArgs& a) {
   // the ping-pong kernel writes one partial per wave row (128 rows), the v2 kernels per tile
   if (a.Co > 128 && !a.r && !a.r2 && conv_nt_pp_ok(a)) return 128;
-  return 256;
+  return v2_small_tile(a) ? 128 : 256;
 }
 
 template <typename E, int ST>
@@ -462,12 +473,16 @@ hipError_t v2_dispatch(int dtype, const ConvArgs& a, hipStream_t s) {
     return v2_launch<E, 256, 4, 2, 2, ST>(a, s);
   }
   if (a.Co > 64) return v2_launch<E, 128, 4, 2, 3, ST>(a, s);
+  if (v2_small_tile(a)) return v2_launch<E, 64, 8, 1, 3, ST, 0, 16, 128>(a, s);
   return v2_launch<E, 64, 8, 1, 3, ST>(a, s);
 }
 
 template <typename E>
 hipError_t nt_v2_e(int dtype, const ConvArgs& a, hipStream_t s) {
-  if (a.tap8) return v2_launch<E, 64, 8, 1, 3, 1, 1>(a, s);
+  if (a.tap8) {
+    if (v2_small_tile(a)) return v2_launch<E, 64, 8, 1, 3, 1, 2, 16, 128>(a, s);
+    return v2_launch<E, 64, 8, 1, 3, 1, 2>(a, s);
+  }
   if (a.st == 1) return v2_dispatch<E, 1>(dtype, a, s);
   if (a.st == 2) return v2_dispatch<E, 2>(dtype, a, s);
   return hipErrorInvalidValue;

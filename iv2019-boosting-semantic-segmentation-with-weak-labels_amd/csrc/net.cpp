@@ -112,13 +112,14 @@ struct seg_ctx {
   // graph
   Act img;                        // compute-dtype images
   int stem = -1;
-  // bf16 stem as 8-channel taps (tap8): padded images [N][H][W][8] and weights [64][stem_ldw]
-  bool stem8 = false;
+  // 16-bit stem as a 4 x 4 conv over the space-to-depth image (conv.h): img [N][Ho+3][Wo+3][16],
+  // weights [64][256] (stem_wpad); img_dbg = the [N][H][W][8] image view for seg_debug_tensor
+  bool stem_s2d = false;
+  void* img_dbg = nullptr;
   FlipJob* flip_jobs = nullptr;   // device table: every dgrad weight flip in one launch
   int n_flip = 0;
   long flip_total = 0;
   bf16_t* stem_wpad = nullptr;
-  int stem_ldw = 0;
   Act z0, dz0, p0, dp0;
   uint8_t* pool_arg = nullptr;    // max-pool first-max window index per output element
   int pool_ph = 0, pool_pw = 0;
@@ -378,13 +379,14 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
 // target ~128 workgroups (half the CUs, the chain keeps the other half: 90.4 -> 92.9 img/s
 // on C2 against 512, and half the split-K slab traffic); alone (profiled, single stream,
 // seg_op_*): ~2 waves of the 256 CUs.
-int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false) {
-  if (!ci) ci = L.ci;   // 8 for the tap8 stem
+int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false, int k = 0) {
+  if (!ci) ci = L.ci;   // 16 for the space-to-depth stem
+  if (!k) k = L.k;      // 4 for the space-to-depth stem
   int BM = L.co_pad <= 64 ? 64 : 128;
   int BN = 128;
   long P = (long)L.N * L.Ho * L.Wo;
-  if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, L.k * L.k * ci, P, &BM, &BN);
-  long tiles = (long)((L.co_pad + BM - 1) / BM) * ((L.k * L.k * ci + BN - 1) / BN);
+  if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, k * k * ci, P, &BM, &BN);
+  long tiles = (long)((L.co_pad + BM - 1) / BM) * ((k * k * ci + BN - 1) / BN);
   // each split >= 32 K-steps of 64 pixels
   const long target = concurrent ? 128 : 512;
   long s = std::max<long>(1, target / std::max<long>(tiles, 1));
@@ -436,13 +438,14 @@ int conv_forward(Step& S, int li, const Act& x) {
   a.y = L.y.p; a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co; a.ldy = L.y.ld;
   a.KH = a.KW = L.k; a.sf = L.stride; a.st = 1; a.pad_h = L.pad_h; a.pad_w = L.pad_w;
   a.dil = L.rate; a.stats = L.stats_part;
-  if (li == c->stem && c->stem8) {
-    a.C = 8; a.ldx = 8; a.tap8 = 1; a.w = c->stem_wpad; a.ldw = c->stem_ldw;
+  if (li == c->stem && c->stem_s2d) {   // 4 x 4 VALID over the space-to-depth image
+    a.C = 16; a.ldx = 16; a.tap8 = 2; a.w = c->stem_wpad; a.ldw = 256;
+    a.KH = a.KW = 4; a.sf = 1; a.pad_h = a.pad_w = 0; a.dil = 1;
   }
   long M = (long)x.N * L.Ho * L.Wo;
   int slot;
   const double esz = c->esz;   // x + w + y, each once
-  const double gbx = ((double)x.N * x.H * x.W * L.ci + (double)L.co * L.k * L.k * L.ci +
+  const double gbx = ((double)L.N * L.H * L.W * L.ci + (double)L.co * L.k * L.k * L.ci +
                       (double)M * L.co) * esz * 1e-9;
   if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot, gbx)) return r;
   HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
@@ -602,24 +605,24 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   a.x = x.p; a.N = x.N; a.H = x.H; a.W = x.W; a.C = x.C; a.ldx = x.ld;
   a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co_pad;
   a.KH = a.KW = L.k; a.sf = L.stride; a.pad_h = L.pad_h; a.pad_w = L.pad_w; a.dil = L.rate;
-  const bool s8 = li == c->stem && c->stem8;
-  if (s8) { a.C = 8; a.ldx = 8; }
+  const bool s2d = li == c->stem && c->stem_s2d;
+  if (s2d) { a.KH = a.KW = 4; a.sf = 1; a.pad_h = a.pad_w = 0; a.dil = 1; }
   // the stem's weight gradient is the last work of the step (its dgrad is skipped): nothing
   // runs beside it, so it takes the whole chip (tools/timeline.py: the compute stream idled
   // ~0.75 ms waiting for it)
-  a.splits = wgrad_splits(L, a.C, c->side_active && li != c->stem);
+  a.splits = wgrad_splits(L, a.C, c->side_active && li != c->stem, a.KH);
   a.out = c->slab;
   long P = (long)L.N * L.Ho * L.Wo;
   int slot;
   // dy + x (16-bit) + the fp32 weight gradient; split-K slab traffic is overhead, not algorithmic
-  const double gbx = (((double)P * L.co + (double)x.N * x.H * x.W * L.ci) * c->esz +
+  const double gbx = (((double)P * L.co + (double)L.N * L.H * L.W * L.ci) * c->esz +
                       (double)L.co * L.k * L.k * L.ci * 4.0) * 1e-9;
   if (int r = prof_begin(c, S.s, 2, li, 2.0 * P * L.co * L.k * L.k * L.ci * 1e-9, &slot, gbx)) return r;
   HIPCALL(c, launch_conv_wgrad(S.dt, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
-  if (s8) {
-    HIPCALL(c, launch_splitk_reduce_pad8(c->slab, a.splits, (long)L.co_pad * L.k * L.k * 8, L.co,
-                                         L.k * L.k, L.ci, c->grads + L.w_off, S.s));
+  if (s2d) {
+    HIPCALL(c, launch_splitk_reduce_s2d(c->slab, a.splits, (long)L.co_pad * 256, L.co,
+                                        c->grads + L.w_off, S.s));
     return 0;
   }
   const long n = (long)L.co * L.k * L.k * L.ci;
@@ -804,13 +807,19 @@ int build(seg_ctx* c) {
 
   // ---- activations ----
   const int H = g.height, W = g.width;
-  // the stem input is context-owned in every dtype (the 16-bit tap-8 image, or an fp32 copy):
-  // the stem's weight gradient reads it in seg_backward, after the caller's buffer may be gone
-  c->stem8 = seg_half(c->dt);
-  if (int r = alloc_act(c, c->img, N, H, W, c->stem8 ? 8 : 3)) return r;
-  c->img.N = N; c->img.H = H; c->img.W = W; c->img.C = 3; c->img.ld = c->stem8 ? 8 : 3;
+  // the stem input is context-owned in every dtype (the 16-bit space-to-depth image, or an fp32
+  // copy): the stem's weight gradient reads it in seg_backward, after the caller's buffer may
+  // be gone
+  c->stem_s2d = seg_half(c->dt);
   ConvL& st = c->convs[c->stem];
   if (int r = alloc_conv(c, st, N, H, W)) return r;
+  if (c->stem_s2d) {
+    if (st.k != 7 || st.stride != 2 || st.ci != 3)
+      return set_err(&c->err, -EINVAL, "space-to-depth stem expects a 7x7/2 conv of 3 channels");
+    if (int r = alloc_act(c, c->img, N, st.Ho + 3, st.Wo + 3, 16)) return r;
+  } else {
+    if (int r = alloc_act(c, c->img, N, H, W, 3)) return r;
+  }
   if (int r = alloc_relu_act(c, c->z0, N, st.Ho, st.Wo, 64)) return r;
   if (int r = alloc_act(c, c->dz0, N, st.Ho, st.Wo, 64)) return r;
   {  // max_pool2d 3x3/2 SAME
@@ -910,14 +919,14 @@ int build(seg_ctx* c) {
       L.wt_lp = p;
     }
     if (seg_half(c->dt)) L.w_lp = (uint16_t*)c->w_lp_flat + L.w_off;   // bf16 or fp16 bits
-    const int wci = (&L == &c->convs[c->stem] && c->stem8) ? 8 : L.ci;
-    const int sp = std::max(wgrad_splits(L, wci, false), wgrad_splits(L, wci, true));
-    slab = std::max(slab, (size_t)sp * L.co_pad * L.k * L.k * wci);
+    const bool s2d = &L == &c->convs[c->stem] && c->stem_s2d;
+    const int wci = s2d ? 16 : L.ci, wk = s2d ? 4 : L.k;
+    const int sp = std::max(wgrad_splits(L, wci, false, wk), wgrad_splits(L, wci, true, wk));
+    slab = std::max(slab, (size_t)sp * L.co_pad * wk * wk * wci);
   }
-  if (c->stem8) {
+  if (c->stem_s2d) {
     const ConvL& st = c->convs[c->stem];
-    c->stem_ldw = (st.k * st.k * 8 + 63) / 64 * 64;
-    if (int r = dalloc(c, &c->stem_wpad, (size_t)st.co * c->stem_ldw)) return r;
+    if (int r = dalloc(c, &c->stem_wpad, (size_t)st.co * 256)) return r;
   }
   c->slab_floats = slab;
   if (int r = dalloc(c, &c->slab, slab)) return r;
@@ -991,8 +1000,10 @@ int forward(Step& S, const float* images) {
   seg_ctx* c = S.c;
   if (c->bn_infer)
     HIPCALL(c, launch_bn_infer_finalize_all(c->infer_jobs, (int)c->convs.size(), S.s));
-  if (c->stem8) {
-    HIPCALL(c, launch_cast_pad8(S.dt, images, c->img.p, c->img.M(), S.s));
+  if (c->stem_s2d) {
+    const ConvL& st = c->convs[c->stem];
+    HIPCALL(c, launch_cast_s2d(S.dt, images, c->img.p, st.N, st.H, st.W, c->img.H, c->img.W, st.pad_h,
+                               st.pad_w, S.s));
   } else {
     HIPCALL(c, hipMemcpyAsync(c->img.p, images, (size_t)c->img.M() * 3 * sizeof(float),
                               hipMemcpyDeviceToDevice, S.s));
@@ -1147,10 +1158,9 @@ int backward_layers(Step& S) {
 }
 
 int refresh_stem_pad(seg_ctx* c, hipStream_t s) {
-  if (!c->stem8) return 0;
+  if (!c->stem_s2d) return 0;
   const ConvL& st = c->convs[c->stem];
-  HIPCALL(c, launch_stem_pad_weights((const bf16_t*)st.w_lp, c->stem_wpad, st.co, st.k * st.k, st.ci,
-                                     c->stem_ldw, s));
+  HIPCALL(c, launch_stem_s2d_weights((const bf16_t*)st.w_lp, c->stem_wpad, st.co, s));
   return 0;
 }
 
@@ -1522,7 +1532,19 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
     size_t us = n.find('_');
     int i = atoi(n.substr(4, us - 4).c_str());
     if (i < 0 || i >= (int)c->convs.size() || us == std::string::npos) return set_err(&c->err, -EINVAL, "bad conv");
-    if (n.substr(us) == "_x") a = c->convs[i].x;
+    if (n.substr(us) == "_x" && i == c->stem && c->stem_s2d) {
+      // the stem reads the space-to-depth image: present the [N][H][W][8] view of it
+      const ConvL& st = c->convs[c->stem];
+      if (!c->img_dbg) {
+        char* p;
+        if (int r = dalloc(c, &p, (size_t)st.N * st.H * st.W * 8 * 2)) return r;
+        c->img_dbg = p;
+      }
+      HIPCALL(c, launch_unshuffle_s2d(c->img.p, c->img_dbg, st.N, st.H, st.W, c->img.H, c->img.W,
+                                      st.pad_h, st.pad_w, 0));
+      HIPCALL(c, hipDeviceSynchronize());
+      a.p = c->img_dbg; a.N = st.N; a.H = st.H; a.W = st.W; a.C = 3; a.ld = 8;
+    } else if (n.substr(us) == "_x") a = c->convs[i].x;
     else if (n.substr(us) == "_y") a = c->convs[i].y;
     else if (n.substr(us) == "_dy") a = c->convs[i].dy;
     else return set_err(&c->err, -EINVAL, "unknown tensor %s", name);
