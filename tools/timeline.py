@@ -8,7 +8,7 @@ from collections import defaultdict
 db = sys.argv[1]
 c = sqlite3.connect(db)
 rows = c.execute("select name, stream_id, queue_id, start, end from kernels order by start").fetchall()
-starts = [r[3] for r in rows if "cast_pad8_kernel" in r[0]]
+starts = [r[3] for r in rows if "cast_s2d_kernel" in r[0] or "cast_pad8_kernel" in r[0]]
 if len(starts) < 3:
     sys.exit("need >= 3 steps")
 # the second-to-last complete step (the last one is the bench's extra mIoU forward)
