@@ -93,6 +93,9 @@ int seg_backward(seg_ctx* ctx, void* stream);
  * grad_scale multiplies the gradient (1/world_size after a SUM all-reduce) */
 int seg_apply_update(seg_ctx* ctx, float lr, float momentum, float ema_decay_eff,
                      float grad_scale, void* stream);
+/* tf.train.MomentumOptimizer(use_nesterov=on) for later updates (define_optimizer.py:17-20):
+ * var -= lr * (g + momentum * accum) instead of var -= lr * accum; off by default */
+int seg_set_nesterov(seg_ctx* ctx, int on);
 
 /* outputs ------------------------------------------------------------------------------
  * losses: device float[10] = {segmentation, l1, l2_vehicle, l2_human, n1, n2v, n2h,
@@ -117,6 +120,14 @@ int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions,
 int seg_set_bn_inference(seg_ctx* ctx, int on);
 int seg_predict(seg_ctx* ctx, const int32_t* cid_map, int n_map, int replace_voids, int out_h,
                 int out_w, int32_t* decisions_out, void* stream);
+/* seg_full_predictions: the model's full-resolution `predictions` of the last seg_forward
+ * (hierarchical.py:84-130) at network resolution H x W, C = c1 + c2 + c3 channels (l1 | l2
+ * vehicle | l2 human): logits_out f32 [N][H][W][C] (align-corners bilinear upsampling of the
+ * low-res logits), probs_out f32 [N][H][W][C] (per-head softmax), head_decisions_out int32
+ * [N][H][W][3] (per-head argmax), decisions_out int32 [N][H][W] (fused, common cids). Every
+ * output is optional (NULL skips it); float outputs 16-byte aligned. */
+int seg_full_predictions(seg_ctx* ctx, float* logits_out, float* probs_out,
+                         int32_t* head_decisions_out, int32_t* decisions_out, void* stream);
 
 /* input preprocessing (input_cityscapes.py:66-96,190-209), after the host
  * decodes TFRecord -> tf.train.Example -> PNG (input_pipelines/tfrecords.py):

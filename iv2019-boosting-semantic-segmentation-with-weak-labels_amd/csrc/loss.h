@@ -50,8 +50,21 @@ struct EvalArgs {
   int* out;                // [N][Ho][Wo]
 };
 
+// Full-resolution predictions of the model (hierarchical.py:84-130) at network resolution;
+// each output is optional (nullptr skips it)
+struct FullPredArgs {
+  const float* logits;     // [N][Hl][Wl][ldl]
+  int N, Hl, Wl, ldl;
+  int H, W;                // network resolution
+  float* logits_out;       // [N][H][W][c1+c2+c3] upsampled logits (l1 | l2v | l2h)
+  float* probs_out;        // [N][H][W][c1+c2+c3] per-head softmax
+  int* head_decs_out;      // [N][H][W][3] per-head argmax (l1, l2v, l2h)
+  int* decs_out;           // [N][H][W] fused decisions in common cids
+};
+
 int loss_head_blocks(int N, int Hl, int Wl);
 hipError_t launch_eval_decisions(const EvalArgs& a, const LossTables& t, hipStream_t s);
+hipError_t launch_full_predictions(const FullPredArgs& a, const LossTables& t, hipStream_t s);
 hipError_t launch_loss_head(const LossArgs& a, const LossTables& t, hipStream_t s);
 // out[0..9] = {seg, l1, l2v, l2h, n1, n2v, n2h, f1, f2v, f2h}; dzscale[ldl] per-channel
 // factors (1/n1 | 0.1/n2v | 0.1/n2h; 0 where the count is 0)

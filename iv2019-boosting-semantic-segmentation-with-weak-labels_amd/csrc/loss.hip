@@ -509,6 +509,81 @@ __global__ __launch_bounds__(256) void eval_decisions_kernel(EvalArgs a, LossTab
     a.out[id] = d;
   }
 }
+// The model's full-resolution `predictions` (hierarchical.py:84-130), materialised on demand:
+// per network-resolution pixel the align-corners bilinear logits of the three heads, their
+// softmax, per-head argmax and the fused common-cid decision. Same arithmetic as the loss
+// head / eval kernel (one thread per pixel, the 4 low-res source cells read through L2); every
+// output is optional. Stores are per pixel runs of CT floats (float4 where CT % 4 == 0).
+template <int C1, int C2, int C3>
+__global__ __launch_bounds__(256) void full_predictions_kernel(FullPredArgs a, LossTables t) {
+  constexpr int CT = C1 + C2 + C3;
+  const long total = (long)a.N * a.H * a.W;
+  for (long id = (long)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+       id += (long)gridDim.x * blockDim.x) {
+    const int w = (int)(id % a.W);
+    const int h = (int)((id / a.W) % a.H);
+    const int n = (int)(id / ((long)a.W * a.H));
+    int ylo, yhi, xlo, xhi;
+    float yl, xl;
+    lerp_of(h, a.Hl, a.H, ylo, yhi, yl);
+    lerp_of(w, a.Wl, a.W, xlo, xhi, xl);
+    const float* base = a.logits + (size_t)n * a.Hl * a.Wl * a.ldl;
+    const float* tl = base + ((size_t)ylo * a.Wl + xlo) * a.ldl;
+    const float* tr = base + ((size_t)ylo * a.Wl + xhi) * a.ldl;
+    const float* bl = base + ((size_t)yhi * a.Wl + xlo) * a.ldl;
+    const float* br = base + ((size_t)yhi * a.Wl + xhi) * a.ldl;
+    float p[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      float top = tl[c] + (tr[c] - tl[c]) * xl;
+      float bot = bl[c] + (br[c] - bl[c]) * xl;
+      p[c] = top + (bot - top) * yl;
+    }
+    auto store = [&](float* dst) {
+      float* o = dst + (size_t)id * CT;
+      if constexpr (CT % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < CT; c += 4)
+          *reinterpret_cast<float4*>(o + c) = make_float4(p[c], p[c + 1], p[c + 2], p[c + 3]);
+      } else {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) o[c] = p[c];
+      }
+    };
+    if (a.logits_out) store(a.logits_out);
+    auto softmax = [&](int c0, int nc) {
+      float m = p[c0];
+#pragma unroll
+      for (int c = 1; c < nc; ++c) m = fmaxf(m, p[c0 + c]);
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < nc; ++c) { p[c0 + c] = __expf(p[c0 + c] - m); s += p[c0 + c]; }
+      const float rs = 1.f / s;
+#pragma unroll
+      for (int c = 0; c < nc; ++c) p[c0 + c] = p[c0 + c] * rs;
+    };
+    softmax(0, C1);
+    softmax(C1, C2);
+    softmax(C1 + C2, C3);
+    if (a.probs_out) store(a.probs_out);
+    auto argmax = [&](int c0, int nc) {   // tf.argmax: first maximum
+      int b = 0;
+      float bv = p[c0];
+#pragma unroll
+      for (int c = 1; c < nc; ++c) if (p[c0 + c] > bv) { bv = p[c0 + c]; b = c; }
+      return b;
+    };
+    const int d1 = argmax(0, C1), dv = argmax(C1, C2), dh = argmax(C1 + C2, C3);
+    if (a.head_decs_out) {
+      int* o = a.head_decs_out + (size_t)id * 3;
+      o[0] = d1; o[1] = dv; o[2] = dh;
+    }
+    if (a.decs_out)
+      a.decs_out[id] = d1 == t.cid_l1_vehicle ? t.veh_to_common[dv]
+                     : d1 == t.cid_l1_human ? t.hum_to_common[dh] : t.l1_to_common[d1];
+  }
+}
+
 __global__ void confusion_global_kernel(const int* __restrict__ lab, const int* __restrict__ dec,
                                         long n, int nc, int* cm) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -567,6 +642,20 @@ hipError_t launch_eval_decisions(const EvalArgs& a, const LossTables& t, hipStre
     hipLaunchKernelGGL((eval_decisions_kernel<14, 7, 3>), dim3((int)g), dim3(256), 0, s, a, t);
   else if (t.c1 == 53 && t.c2 == 12 && t.c3 == 5)
     hipLaunchKernelGGL((eval_decisions_kernel<53, 12, 5>), dim3((int)g), dim3(256), 0, s, a, t);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_full_predictions(const FullPredArgs& a, const LossTables& t, hipStream_t s) {
+  const long total = (long)a.N * a.H * a.W;
+  if (total <= 0) return hipSuccess;
+  long g = (total + 255) / 256;
+  if (g > 16384) g = 16384;
+  if (t.c1 == 14 && t.c2 == 7 && t.c3 == 3)
+    hipLaunchKernelGGL((full_predictions_kernel<14, 7, 3>), dim3((int)g), dim3(256), 0, s, a, t);
+  else if (t.c1 == 53 && t.c2 == 12 && t.c3 == 5)
+    hipLaunchKernelGGL((full_predictions_kernel<53, 12, 5>), dim3((int)g), dim3(256), 0, s, a, t);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -166,6 +166,7 @@ struct seg_ctx {
   int sync_world = 1;
   float* sync_pack = nullptr;     // [2 * max C]
   float loss_scale = 1.f;         // gradient seed multiplier (fp16 dynamic loss scaling)
+  int nesterov = 0;               // MomentumOptimizer use_nesterov (seg_set_nesterov)
   int* skip_flag = nullptr;       // device: non-finite scaled gradients this step (update skipped)
   bool side_on = false;
   bool side_active = false;        // this backward: side_on and not profiling (kernel-alone timing)
@@ -1354,6 +1355,20 @@ int seg_predict(seg_ctx* c, const int32_t* cid_map, int n_map, int replace_voids
   return 0;
 }
 
+int seg_full_predictions(seg_ctx* c, float* logits_out, float* probs_out,
+                         int32_t* head_decisions_out, int32_t* decisions_out, void* stream) {
+  NEED_BOUND(c);
+  FullPredArgs a{};
+  a.logits = (const float*)c->logits.p; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
+  a.ldl = c->ldl; a.H = c->cfg.height; a.W = c->cfg.width;
+  a.logits_out = logits_out; a.probs_out = probs_out;
+  a.head_decs_out = head_decisions_out; a.decs_out = decisions_out;
+  if ((reinterpret_cast<uintptr_t>(logits_out) | reinterpret_cast<uintptr_t>(probs_out)) & 15)
+    return set_err(&c->err, -EINVAL, "logits_out / probs_out must be 16-byte aligned");
+  HIPCALL(c, launch_full_predictions(a, c->tables, (hipStream_t)stream));
+  return 0;
+}
+
 int seg_backward(seg_ctx* c, void* stream) {
   NEED_BOUND(c);
   Step S{c, (hipStream_t)stream, c->dt};
@@ -1378,7 +1393,7 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
   a.lp_f16 = c->dt == SEG_F16;
   a.skip = c->skip_flag;
   a.n = c->n_decay; a.lr = lr; a.momentum = momentum; a.wd = c->cfg.weight_decay;
-  a.ema_decay = ema_decay_eff; a.reg_part = c->reg_part;
+  a.ema_decay = ema_decay_eff; a.reg_part = c->reg_part; a.nesterov = c->nesterov;
   HIPCALL(c, launch_sgdm(a, s));
   HIPCALL(c, launch_sum_partials(c->reg_part, sgdm_blocks(c->n_decay), c->reg_out, s));
   if (c->cfg.train_bn) {
@@ -1413,6 +1428,12 @@ int seg_confusion(seg_ctx* c, const int32_t* labels, const int32_t* decisions, i
   hipError_t e = hipMemsetAsync(cm, 0, (size_t)num_classes * num_classes * 4, s);
   if (e == hipSuccess) e = launch_confusion(labels, decisions, n, num_classes, cm, s);
   if (e != hipSuccess) return hip_fail(c, e, "seg_confusion");
+  return 0;
+}
+
+int seg_set_nesterov(seg_ctx* c, int on) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  c->nesterov = on ? 1 : 0;
   return 0;
 }
 

@@ -15,6 +15,7 @@ struct SgdmArgs {
   float lr, momentum, wd, ema_decay;
   float* reg_part;     // optional [blocks] partial sums of 0.5*wd*w_old^2
   const int* skip;     // optional device flag: != 0 = non-finite gradients, keep the weights
+  int nesterov;        // MomentumOptimizer(use_nesterov=True): var -= lr * (g + m * accum)
 };
 
 int sgdm_blocks(long n);

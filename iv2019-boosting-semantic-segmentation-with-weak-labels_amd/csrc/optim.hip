@@ -18,10 +18,11 @@ __global__ void sgdm_kernel(SgdmArgs a) {
     if (skip) continue;
     // total gradient = d(seg)/dw + d(wd * sum(w^2)/2)/dw
     const float gt = a.g[i] + a.wd * w_old;
-    // tf.train.MomentumOptimizer (use_nesterov=False): accum = accum*m + g; var -= lr*accum
+    // tf.train.MomentumOptimizer: accum = accum*m + g; var -= lr*accum, or with
+    // use_nesterov var -= lr*(g + m*accum) (training_ops ApplyMomentum)
     const float v = a.v[i] * a.momentum + gt;
     a.v[i] = v;
-    const float w_new = w_old - a.lr * v;
+    const float w_new = a.nesterov ? w_old - a.lr * (gt + a.momentum * v) : w_old - a.lr * v;
     a.w[i] = w_new;
     if (a.ema) a.ema[i] -= (1.f - a.ema_decay) * (a.ema[i] - w_old);
     if (a.w_lp) {

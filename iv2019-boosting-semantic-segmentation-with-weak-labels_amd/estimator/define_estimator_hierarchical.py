@@ -102,6 +102,8 @@ def define_estimator(mode, features, labels, model_fn, config, params):
         ctx._scaler = DynamicLossScaler(ctx)
     losses = define_losses(mode, predictions, labels, config, params)
     optimizer = define_optimizer(global_step, params)
+    if getattr(ctx, 'nesterov', False) != optimizer.use_nesterov:
+        ctx.set_nesterov(optimizer.use_nesterov)
 
     def train_op():
         ctx.backward()
@@ -135,7 +137,7 @@ def _eval_spec(predictions, labels, config, params):
     nc = max(_replacevoids(tcids2ecids)) + 1
     cm = torch.empty((nc, nc), dtype=torch.int32, device=prolabels.device)
     ctx.confusion(prolabels.to(torch.int32).contiguous(), decs, nc, cm)
-    out = dict(predictions)
+    out = predictions.materialised() if hasattr(predictions, 'materialised') else dict(predictions)
     out['decisions'] = decs
     return EstimatorSpec(ModeKeys.EVAL, out, losses['total'], None, losses,
                          {'confusion_matrix': cm})
@@ -147,8 +149,8 @@ def _predict_spec(predictions, features, params):
     (height_system, width_system) when both are set, else to the raw image size, else kept at
     network resolution (_resize_predictions, nearest align-corners); --replace_voids runs on
     the device only where that resize is the identity (the reference replaces voids on
-    bilinearly resized probabilities). The low-resolution logits stand in for the
-    full-resolution probabilities, which the fused head never materialises."""
+    bilinearly resized probabilities). The full-resolution logits / probabilities / per-head
+    decisions stay lazy entries of the model's predictions (materialised on first access)."""
     import torch
     ctx = predictions['_context']
     img = features['proimages']
@@ -163,8 +165,7 @@ def _predict_spec(predictions, features, params):
                                   'network size (bilinear probability resize) is not built')
     decs = torch.empty((n,) + tuple(size), dtype=torch.int32, device=img.device)
     ctx.predict(list(range(params.output_Nclasses)), decs, replace_voids=replace)
-    out = {k: v for k, v in predictions.items()
-           if k in ('l1_logits', 'l2_vehicle_logits', 'l2_human_logits', '_context')}
+    out = predictions
     out['decisions'] = decs
     for k in ('rawimages', 'rawimagespaths'):
         if k in features:

@@ -1,8 +1,8 @@
 """Learning-rate schedules + optimizer selection, drop-in for estimator/define_optimizer.py.
 
 The update itself is the fused HIP kernel (``seg_apply_update``); this module resolves the
-per-step learning rate exactly as tf.train.piecewise_constant / polynomial_decay do, and the
-momentum (MomentumOptimizer) or 0 (GradientDescentOptimizer).
+per-step learning rate exactly as tf.train.piecewise_constant / polynomial_decay do, the
+momentum (MomentumOptimizer, optionally Nesterov) or 0 (GradientDescentOptimizer).
 """
 from dataclasses import dataclass
 from typing import List
@@ -39,8 +39,6 @@ class Optimizer:
 
 
 def define_optimizer(global_step, params):
-    if params.use_nesterov if hasattr(params, 'use_nesterov') else False:
-        raise NotImplementedError('use_nesterov: the fused update implements plain momentum only')
     if params.learning_rate_schedule not in ('piecewise_constant', 'polynomial_decay'):
         print('Unknown option for learning rate schedule.')
     if params.optimizer == 'SGDM':
@@ -55,7 +53,8 @@ def define_optimizer(global_step, params):
                      initial=params.learning_rate_initial,
                      final=params.learning_rate_final, power=params.learning_rate_power,
                      decay_steps=max(int(getattr(params, 'num_training_steps', 1)), 1),
-                     momentum=momentum, use_nesterov=False)
+                     momentum=momentum,
+                     use_nesterov=params.optimizer == 'SGDM' and bool(getattr(params, 'use_nesterov', False)))
 
 
 class DynamicLossScaler:

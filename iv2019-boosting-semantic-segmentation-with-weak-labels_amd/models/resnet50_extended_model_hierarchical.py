@@ -7,14 +7,20 @@ dilated ResNet-50/101 encoder, the PSP pyramid, the three adaptation bottlenecks
 logits convs, and this function runs its forward pass on the device tensor ``features``
 (``proimages``, NHWC fp32 in [-1, 1)).
 
-``predictions`` carries the LOW-RESOLUTION logits (the 8x align-corners upsampling of
-hierarchical.py:84-86 is fused into the loss head, which never materialises full-resolution
-logits); in TRAIN ``decisions`` is the full-resolution fused decision map filled by the loss
-head; in EVAL / PREDICT ``decisions`` is produced by ``seg_predict`` (no loss head) from the
-logits of a forward whose batch norm uses the moving statistics unless
+``predictions`` has the reference's keys (hierarchical.py:121-130): ``l1_logits``,
+``l1_probabilities``, ``l1_decisions`` and the same for ``l2_vehicle`` / ``l2_human`` at full
+network resolution (NHWC), and ``decisions``. The training step never needs the
+full-resolution tensors (the 8x align-corners upsampling of hierarchical.py:84-86, the softmax
+and the argmax are fused into the loss head), so they are materialised on first access by one
+``seg_full_predictions`` launch and cached; the low-resolution logits the network produces are
+under ``*_logits_lowres``. In TRAIN ``decisions`` is the full-resolution fused decision map
+filled by the loss head; in EVAL / PREDICT it is produced by ``seg_predict`` (no loss head)
+from the logits of a forward whose batch norm uses the moving statistics unless
 ``batch_norm_accumulate_statistics`` is set (hierarchical.py:306-307).
 """
 from __future__ import annotations
+
+from collections.abc import MutableMapping
 
 import numpy as np
 
@@ -106,17 +112,77 @@ def model(mode, features, labels, config, params):
     if getattr(ctx, 'bn_inference', False) != infer:
         ctx.set_bn_inference(infer)
     ctx.forward(features.contiguous())
-    _, _, logits = ctx.outputs()
-    c1, c2, c3 = (53, 12, 5) if params.per_pixel_dataset_name == 'vistas' else (14, 7, 3)
-    n = features.shape[0]
-    decisions = torch.zeros((n, params.height_feature_extractor, params.width_feature_extractor),
-                            dtype=torch.int32, device=features.device)
-    predictions = {'l1_logits': logits[..., :c1],
-                   'l2_vehicle_logits': logits[..., c1:c1 + c2],
-                   'l2_human_logits': logits[..., c1 + c2:c1 + c2 + c3],
-                   'decisions': decisions,
-                   '_context': ctx}
-    return None, {}, predictions
+    return None, {}, Predictions(ctx, params.per_pixel_dataset_name)
+
+
+HEADS = ('l1', 'l2_vehicle', 'l2_human')
+LAZY_KEYS = tuple(f'{h}_{k}' for h in HEADS for k in ('logits', 'probabilities', 'decisions'))
+
+
+class Predictions(MutableMapping):
+    """The model's ``predictions`` (hierarchical.py:121-130) for the last forward of ``ctx``.
+
+    Eager entries: ``decisions`` (int32 [N, H, W]; filled by the loss head in TRAIN),
+    ``*_logits_lowres`` (zero-copy views of the network's output, [N, H/8, W/8, c]) and
+    ``_context``. The nine full-resolution entries of LAZY_KEYS are produced together by one
+    ``seg_full_predictions`` launch on first access (f32 [N, H, W, c] logits and
+    probabilities, int32 [N, H, W] decisions); reading them after the context has run another
+    forward raises instead of returning the newer forward's values."""
+
+    def __init__(self, ctx, dataset='cityscapes'):
+        import torch
+        self._ctx = ctx
+        self._forward_id = getattr(ctx, 'forward_count', 0)
+        self._c = (53, 12, 5) if dataset == 'vistas' else (14, 7, 3)
+        _, _, logits = ctx.outputs()
+        n, h, w = logits.shape[0], ctx.cfg.height, ctx.cfg.width
+        self._shape = (n, h, w)
+        c1, c2, c3 = self._c
+        self._store = {'decisions': torch.zeros((n, h, w), dtype=torch.int32, device=logits.device),
+                       'l1_logits_lowres': logits[..., :c1],
+                       'l2_vehicle_logits_lowres': logits[..., c1:c1 + c2],
+                       'l2_human_logits_lowres': logits[..., c1 + c2:c1 + c2 + c3],
+                       '_context': ctx}
+
+    def _materialise(self):
+        import torch
+        if getattr(self._ctx, 'forward_count', 0) != self._forward_id:
+            raise RuntimeError('full-resolution predictions requested after the context ran '
+                               'another forward: they are computed from the last forward only')
+        n, h, w = self._shape
+        ct = sum(self._c)
+        dev = self._store['decisions'].device
+        logits = torch.empty((n, h, w, ct), dtype=torch.float32, device=dev)
+        probs = torch.empty_like(logits)
+        hd = torch.empty((n, h, w, 3), dtype=torch.int32, device=dev)
+        self._ctx.full_predictions(logits, probs, hd)
+        lo = 0
+        for i, (head, c) in enumerate(zip(HEADS, self._c)):
+            self._store[f'{head}_logits'] = logits[..., lo:lo + c]
+            self._store[f'{head}_probabilities'] = probs[..., lo:lo + c]
+            self._store[f'{head}_decisions'] = hd[..., i]
+            lo += c
+
+    def __getitem__(self, k):
+        if k in LAZY_KEYS and k not in self._store:
+            self._materialise()
+        return self._store[k]
+
+    def __setitem__(self, k, v):
+        self._store[k] = v
+
+    def __delitem__(self, k):
+        del self._store[k]
+
+    def __iter__(self):
+        return iter(list(dict.fromkeys(LAZY_KEYS + tuple(self._store))))
+
+    def __len__(self):
+        return len(set(LAZY_KEYS) | set(self._store))
+
+    def materialised(self):
+        """The entries computed so far (no launch): a plain dict."""
+        return dict(self._store)
 
 
 def add_model_arguments(argparser):

@@ -26,7 +26,8 @@ EXPORTED_SYMBOLS = [
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
-    "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict",
+    "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict", "seg_full_predictions",
+    "seg_set_nesterov",
     "seg_crc32c", "seg_prepare_images", "seg_prepare_labels",
 ]
 
@@ -111,6 +112,8 @@ def _load():
                                     vp, vp]),
         "seg_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, vp, ctypes.c_size_t]),
         "seg_predict": (ip, [vp, ctypes.POINTER(ctypes.c_int32), ip, ip, ip, ip, vp, vp]),
+        "seg_full_predictions": (ip, [vp, vp, vp, vp, vp, vp]),
+        "seg_set_nesterov": (ip, [vp, ip]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -227,6 +230,7 @@ class SegContext:
     # ---- step -----------------------------------------------------------------------
     def forward(self, images, stream=None):
         check(LIB.seg_forward(self.h, _ptr(images), _stream(stream)), self.h)
+        self.forward_count = getattr(self, "forward_count", 0) + 1
 
     def loss(self, px_labels=None, bbox_soft=None, tag_soft=None, decisions=None, stream=None):
         check(LIB.seg_loss(self.h, _ptr(px_labels), _ptr(bbox_soft), _ptr(tag_soft),
@@ -251,6 +255,29 @@ class SegContext:
         check(LIB.seg_predict(self.h, m, len(cid_map), 1 if replace_voids else 0,
                               int(out.shape[1]), int(out.shape[2]), _ptr(out), _stream(stream)),
               self.h)
+
+    def full_predictions(self, logits=None, probs=None, head_decisions=None, decisions=None,
+                         stream=None):
+        """The model's full-resolution predictions of the last forward at network resolution
+        (hierarchical.py:84-130) written into the given device buffers (any may be None):
+        logits / probs f32 [N, H, W, C] (C = c1 + c2 + c3, heads l1 | l2v | l2h),
+        head_decisions int32 [N, H, W, 3], decisions int32 [N, H, W] (fused, common cids)."""
+        import torch
+        n = self.cfg.nb_pp + self.cfg.nb_pb + self.cfg.nb_pi
+        hw = (self.cfg.height, self.cfg.width)
+        for t, dt, tail in ((logits, torch.float32, None), (probs, torch.float32, None),
+                            (head_decisions, torch.int32, (3,)), (decisions, torch.int32, ())):
+            if t is None:
+                continue
+            if tail is None:
+                tail = (sum((53, 12, 5) if self.cfg.dataset == DATASET["vistas"] else (14, 7, 3)),)
+            ok = (t.dtype == dt and t.is_cuda and t.is_contiguous() and tuple(t.shape[:3]) == (n,) + hw
+                  and tuple(t.shape[3:]) == tail)
+            if not ok:
+                raise ValueError(f"prediction buffer {tuple(t.shape)} {t.dtype}: expected a "
+                                 f"contiguous device tensor [{n}, {hw[0]}, {hw[1]}, ...]")
+        check(LIB.seg_full_predictions(self.h, _ptr(logits), _ptr(probs), _ptr(head_decisions),
+                                       _ptr(decisions), _stream(stream)), self.h)
 
     def backward(self, stream=None):
         check(LIB.seg_backward(self.h, _stream(stream)), self.h)
@@ -308,6 +335,11 @@ class SegContext:
     def wait_bucket(self, i, stream):
         """Make `stream` wait until the last seg_backward has written bucket i."""
         check(LIB.seg_stream_wait_bucket(self.h, i, _stream(stream)), self.h)
+
+    def set_nesterov(self, on: bool):
+        """MomentumOptimizer(use_nesterov=on) for the following updates."""
+        check(LIB.seg_set_nesterov(self.h, 1 if on else 0), self.h)
+        self.nesterov = bool(on)
 
     def apply_update(self, lr, momentum=0.9, ema_decay_eff=0.0, grad_scale=1.0, stream=None):
         check(LIB.seg_apply_update(self.h, lr, momentum, ema_decay_eff, grad_scale,

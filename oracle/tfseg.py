@@ -591,8 +591,10 @@ class OracleNet:
 
     # -- one full training step ----------------------------------------------------------
     def train_step(self, images, px_labels, bbox_soft=None, tag_soft=None, lr=0.01,
-                   momentum=0.9, mom_state=None, ema_state=None, ema_decay=0.0, step=0):
-        """Forward, losses, autodiff backward of the segmentation loss, SGDM with L2 term.
+                   momentum=0.9, mom_state=None, ema_state=None, ema_decay=0.0, step=0,
+                   nesterov=False):
+        """Forward, losses, autodiff backward of the segmentation loss, SGDM with L2 term
+        (MomentumOptimizer, use_nesterov per define_optimizer.py:17-20).
 
         Returns (losses, grads-of-seg-loss, new params, new momentum, new ema, batch stats).
         """
@@ -600,7 +602,8 @@ class OracleNet:
         low = self.forward(torch.as_tensor(images))
         L = self.losses(low, px_labels, bbox_soft, tag_soft)
         return (L, low) + self._grads_and_update(L["segmentation"], trainable, lr, momentum,
-                                                 mom_state, ema_state, ema_decay, step)
+                                                 mom_state, ema_state, ema_decay, step,
+                                                 nesterov)
 
     def train_step_replicas(self, batches, lr=0.01, momentum=0.9):
         """One data-parallel step of R replicas with cross-replica BN (--cross_replica_norm):
@@ -635,7 +638,7 @@ class OracleNet:
         return trainable
 
     def _grads_and_update(self, loss, trainable, lr, momentum, mom_state, ema_state, ema_decay,
-                          step):
+                          step, nesterov=False):
         names = list(trainable)
         grads = torch.autograd.grad(loss, [trainable[n] for n in names], allow_unused=True)
         g = {n: (gr if gr is not None else torch.zeros_like(trainable[n])).detach()
@@ -648,9 +651,10 @@ class OracleNet:
         for n in names:
             w = self.p[n].detach()
             gt = g[n] + (self.cfg.weight_decay * w if n.endswith("/weights") else 0.0)
-            v = momentum * mom_state[n] + gt                 # MomentumOptimizer (no nesterov)
+            v = momentum * mom_state[n] + gt                 # MomentumOptimizer accum
             new_m[n] = v
-            new_p[n] = w - lr * v
+            # ApplyMomentum: var -= lr * accum, or lr * (g + momentum * accum) with use_nesterov
+            new_p[n] = w - lr * (gt + momentum * v) if nesterov else w - lr * v
             if ema_decay > 0:
                 s = (ema_state or {}).get(n, w)
                 new_e[n] = s - (1.0 - d) * (s - w)

@@ -271,3 +271,52 @@ def test_predict_script_exports(cuda, tmp_path, init_ckpt):
         col = np.asarray(Image.open(rdir / f"img{i}_result_color.png"))
         assert lids.shape == (50, 90) and col.shape == (50, 90, 3)
         assert (rdir / f"img{i}_result_overlapped_color.png").exists()
+
+
+@pytest.mark.parametrize("dataset", ["cityscapes", "vistas"])
+def test_model_predictions_full_resolution(cuda, dataset):
+    """model()'s predictions carry the reference's ten keys (hierarchical.py:121-130) at full
+    network resolution: upsampled logits, per-head softmax and argmax, fused decisions. The
+    oracle's head_predictions is fed the NATIVE low-res logits so the upsample / softmax /
+    argmax / fusion is checked by itself: logits and probabilities 1e-5 relative, decisions
+    equal up to fp32 near-ties (<= 0.1 % of the pixels)."""
+    import argparse
+    from input_pipelines.synthetic import batch
+    from models.resnet50_extended_model_hierarchical import (LAZY_KEYS, model,
+                                                             release_contexts)
+    from estimator.mode_keys import ModeKeys
+    h, w, nb = 48, 64, 2
+    s = argparse.Namespace(Nb=nb, height_feature_extractor=h, width_feature_extractor=w,
+                           per_pixel_dataset_name=dataset, compute_dtype="fp32",
+                           pyramid="none", name_feature_extractor="resnet_v1_50")
+    data = batch(21, nb, 0, 0, h, w)
+    release_contexts()
+    _, _, pred = model(ModeKeys.EVAL, torch.as_tensor(data["images"]).to(cuda), None, None, s)
+    assert set(LAZY_KEYS) | {"decisions"} <= set(pred.keys())
+    assert "l1_logits" not in pred.materialised()          # lazy until asked for
+    c = (53, 12, 5) if dataset == "vistas" else (14, 7, 3)
+    low_nat = {k: pred[f"{k}_lowres"].cpu().permute(0, 3, 1, 2).contiguous()
+               for k in ("l1_logits", "l2_vehicle_logits", "l2_human_logits")}
+    cfg = SegConfig(height=h, width=w, nb_pp=nb, pyramid="none", dataset=dataset)
+    net = OracleNet(cfg, init_params(cfg, seed=0), dtype=torch.float32)
+    up, probs, decs, fused = net.head_predictions(low_nat)
+    for head, ci in zip(("l1", "l2_vehicle", "l2_human"), c):
+        lg = pred[f"{head}_logits"]
+        assert tuple(lg.shape) == (nb, h, w, ci)
+        assert _rel(lg.cpu().numpy(), up[f"{head}_logits"].permute(0, 2, 3, 1).numpy()) < 1e-5
+        pr = pred[f"{head}_probabilities"].cpu().numpy()
+        assert _rel(pr, probs[f"{head}_logits"].permute(0, 2, 3, 1).numpy()) < 1e-5
+        np.testing.assert_allclose(pr.sum(-1), 1.0, atol=1e-5)
+        d = pred[f"{head}_decisions"].cpu().numpy()
+        assert d.dtype == np.int32 and d.shape == (nb, h, w)
+        assert float(np.mean(d != decs[f"{head}_logits"].numpy())) <= 1e-3
+    # fused decisions (common cids) through the C ABI's optional decisions output
+    fd = torch.full((nb, h, w), -1, dtype=torch.int32, device=cuda)
+    pred["_context"].full_predictions(decisions=fd)
+    assert float(np.mean(fd.cpu().numpy() != fused.numpy())) <= 1e-3
+    # a newer forward invalidates the lazy entries not yet materialised
+    _, _, pred2 = model(ModeKeys.EVAL, torch.as_tensor(data["images"]).to(cuda), None, None, s)
+    model(ModeKeys.EVAL, torch.as_tensor(data["images"]).to(cuda), None, None, s)
+    with pytest.raises(RuntimeError):
+        pred2["l1_probabilities"]
+    release_contexts()

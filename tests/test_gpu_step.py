@@ -194,10 +194,12 @@ def test_bf16_step_is_deterministic(cuda):
         assert np.array_equal(a["params"][k], b["params"][k]), k
 
 
-def test_two_step_fp32(cuda):
+@pytest.mark.parametrize("nesterov", [False, True], ids=["momentum", "nesterov"])
+def test_two_step_fp32(cuda, nesterov):
     """Step 2 starts from the native step-1 state: its forward (losses, logits) matches the
     oracle run on the same parameters at 1e-3, and the momentum recursion
-    v2 = 0.9 v1 + g2 + wd w1, w2 = w1 - lr v2 holds on the native gradients."""
+    v2 = 0.9 v1 + g2 + wd w1, w2 = w1 - lr v2 (use_nesterov: w2 = w1 - lr (g2 + wd w1 + 0.9 v2),
+    define_optimizer.py:17-20) holds on the native gradients."""
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     cfg = SegConfig(height=64, width=128, nb_pp=2, pyramid="psp")
@@ -206,6 +208,7 @@ def test_two_step_fp32(cuda):
     d2 = batch(22, cfg.nb_pp, 0, 0, cfg.height, cfg.width)
     ctx = SegContext(pyramid="psp", height=64, width=128, nb_pp=2, dtype="fp32")
     ctx.load_params(params)
+    ctx.set_nesterov(nesterov)
     lr = 0.01
     ctx.forward(torch.as_tensor(d1["images"]).to(cuda))
     ctx.loss(torch.as_tensor(d1["px"]).to(cuda))
@@ -233,8 +236,10 @@ def test_two_step_fp32(cuda):
     for k in g2:
         wd = cfg.weight_decay if k.endswith("/weights") else 0.0
         w1 = p1[k].astype(np.float64)
-        v2 = 0.9 * v1[k].astype(np.float64) + g2[k].astype(np.float64) + wd * w1
-        assert _rel(p2[k], w1 - lr * v2) < 1e-5, k
+        gt = g2[k].astype(np.float64) + wd * w1
+        v2 = 0.9 * v1[k].astype(np.float64) + gt
+        exp = w1 - lr * (gt + 0.9 * v2) if nesterov else w1 - lr * v2
+        assert _rel(p2[k], exp) < 1e-5, k
 
 
 def _bn_bwd_ref(dz, y, z, gamma, eps=1.001e-5):

@@ -47,8 +47,9 @@ def _rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-@pytest.mark.parametrize("mix", [(2, 0, 0), (2, 1, 1)], ids=["strong", "strong-bbox-tag"])
-def test_train_main_matches_oracle_trajectory(cuda, tmp_path, capsys, mix):
+@pytest.mark.parametrize("mix,nesterov", [((2, 0, 0), False), ((2, 1, 1), False), ((2, 0, 0), True)],
+                         ids=["strong", "strong-bbox-tag", "strong-nesterov"])
+def test_train_main_matches_oracle_trajectory(cuda, tmp_path, capsys, mix, nesterov):
     import train
     from estimator.define_estimator_hierarchical import get_or_create_global_step
     from input_pipelines.synthetic import batch
@@ -62,6 +63,8 @@ def test_train_main_matches_oracle_trajectory(cuda, tmp_path, capsys, mix):
             "--Nb_per_pixel", str(npp), "--Nb_per_bbox", str(npb), "--Nb_per_image", str(npi),
             "--learning_rate_initial", "1e-5",
             "--save_summaries_steps", "1", "--save_checkpoints_steps", "100"]
+    if nesterov:   # MomentumOptimizer(use_nesterov=True), define_optimizer.py:17-20
+        argv.append("--use_nesterov")
     assert train.main(argv) == 3
     out = capsys.readouterr().out
     logged = [tuple(float(v) for v in m) for m in
@@ -84,7 +87,8 @@ def test_train_main_matches_oracle_trajectory(cuda, tmp_path, capsys, mix):
             net = OracleNet(cfg, params, dtype=dtype)
             L, _, _, new_p, mom, ema, _ = net.train_step(d["images"], d["px"], d["bbox"], d["tag"],
                                                          lr=lr, mom_state=mom, ema_state=ema,
-                                                         ema_decay=0.9, step=k)
+                                                         ema_decay=0.9, step=k,
+                                                         nesterov=nesterov)
             losses.append(tuple(float(L[n].detach()) for n in (
                 "total", "l1_segmentation", "l2_vehicle_segmentation", "l2_human_segmentation")))
             params = {n: v.detach().numpy() for n, v in new_p.items()}
