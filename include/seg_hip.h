@@ -57,6 +57,8 @@ typedef struct seg_cfg {
   float bn_decay;       /* batch_norm_decay (0.9) */
   int train_bn;         /* norm_train_variables */
   float weight_decay;   /* regularization_weight (0.00017): l2_regularizer scale */
+  int fov_k, fov_rate;  /* fov_expansion_kernel_size / _rate: the optional extension/increase_fov
+                           conv (resnet50_extended_feature_extractor.py:44-49); 0 = off */
 } seg_cfg;
 
 /* lifecycle -------------------------------------------------------------------------- */

@@ -125,7 +125,9 @@ struct seg_ctx {
   int pool_ph = 0, pool_pw = 0;
   std::vector<Unit> units;
   int dfd = -1;
-  Act z_dfd, dz_dfd;              // z_dfd may be a slice of concat
+  Act z_dfd, dz_dfd;              // extension output (pyramid input); may be a slice of concat
+  int fov = -1;                   // optional extension/increase_fov conv after decrease_fdims
+  Act z_pre, dz_pre;              // decrease_fdims BN/ReLU output when fov >= 0
   // pyramid
   std::vector<int> pyr_conv;      // per branch conv index
   std::vector<int> pyr_k;         // grid size per branch
@@ -737,6 +739,11 @@ int build(seg_ctx* c) {
     c->units.push_back(u);
   }
   c->dfd = add_conv(c, "feature_extractor/extension/decrease_fdims", 2048, fd, 1, 1, 1, false, true);
+  if (g.fov_k < 0 || g.fov_rate < 0 || (g.fov_k > 0) != (g.fov_rate > 0))
+    return set_err(&c->err, -EINVAL, "fov_k and fov_rate must both be set (hierarchical.py:272-274)");
+  if (g.fov_k > 0)   // slim.conv2d(fe, fd, fov_k, rate=fov_rate): SAME, BN, ReLU
+    c->fov = add_conv(c, "feature_extractor/extension/increase_fov", fd, fd, g.fov_k, 1, g.fov_rate,
+                      false, true);
   if (g.pyramid == SEG_PYRAMID_PSP) {
     const char* nm[4] = {"Conv", "Conv_1", "Conv_2", "Conv_3"};
     for (int i = 0; i < 4; ++i)
@@ -840,6 +847,11 @@ int build(seg_ctx* c) {
   if (int r = alloc_conv(c, dfd, N, x.H, x.W)) return r;
   const int Hf = dfd.Ho, Wf = dfd.Wo;
   if (int r = alloc_act(c, c->dz_dfd, N, Hf, Wf, fd)) return r;
+  if (c->fov >= 0) {
+    if (int r = alloc_relu_act(c, c->z_pre, N, Hf, Wf, fd)) return r;
+    if (int r = alloc_act(c, c->dz_pre, N, Hf, Wf, fd)) return r;
+    if (int r = alloc_conv(c, c->convs[c->fov], N, Hf, Wf)) return r;
+  }
   if (g.pyramid == SEG_PYRAMID_PSP) {
     if (int r = alloc_act(c, c->concat, N, Hf, Wf, 5 * fd)) return r;
     if (int r = alloc_act(c, c->dconcat, N, Hf, Wf, 5 * fd)) return r;
@@ -1017,7 +1029,13 @@ int forward(Step& S, const float* images) {
   for (auto& u : c->units)
     if (int r = unit_forward(S, u)) return r;
   if (int r = conv_forward(S, c->dfd, c->units.back().out)) return r;
-  if (int r = bn_apply(S, c->dfd, c->z_dfd, 0)) return r;
+  if (c->fov >= 0) {
+    if (int r = bn_apply(S, c->dfd, c->z_pre, 0)) return r;
+    if (int r = conv_forward(S, c->fov, c->z_pre)) return r;
+    if (int r = bn_apply(S, c->fov, c->z_dfd, 0)) return r;
+  } else if (int r = bn_apply(S, c->dfd, c->z_dfd, 0)) {
+    return r;
+  }
   if (c->cfg.pyramid == SEG_PYRAMID_PSP) {
     const Act& z = c->z_dfd;
     HIPCALL(c, launch_grid_rowreduce(S.dt, z.p, z.N, z.H, z.W, z.C, z.ld, c->pool_grids,
@@ -1144,7 +1162,14 @@ int backward_layers(Step& S) {
     HIPCALL(c, launch_psp_input_bwd(S.dt, c->dz_dfd.p, c->dz_dfd.ld, c->pool_grids, dps, c->dz_dfd.N,
                                     c->dz_dfd.H, c->dz_dfd.W, fd, c->dz_dfd.p, c->dz_dfd.ld, S.s));
   }
-  if (int r = bn_backward(S, c->dfd, c->dz_dfd, 0, &c->z_dfd, nullptr)) return r;
+  if (c->fov >= 0) {
+    if (int r = bn_backward(S, c->fov, c->dz_dfd, 0, &c->z_dfd, nullptr)) return r;
+    if (int r = conv_wgrad(S, c->fov, c->z_pre)) return r;
+    if (int r = conv_dgrad(S, c->fov, c->dz_pre)) return r;
+    if (int r = bn_backward(S, c->dfd, c->dz_pre, 0, &c->z_pre, nullptr)) return r;
+  } else if (int r = bn_backward(S, c->dfd, c->dz_dfd, 0, &c->z_dfd, nullptr)) {
+    return r;
+  }
   if (int r = conv_wgrad(S, c->dfd, c->units.back().out)) return r;
   if (int r = conv_dgrad(S, c->dfd, c->units.back().dout)) return r;
   for (int i = (int)c->units.size() - 1; i >= 0; --i) {

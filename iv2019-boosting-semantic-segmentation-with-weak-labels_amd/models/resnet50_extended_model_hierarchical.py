@@ -37,8 +37,6 @@ def _validate_params(params):
             getattr(params, 'fov_expansion_kernel_size', 0)):
         raise ValueError("One of params.{fov_expansion_kernel_rate, fov_expansion_kernel_size} "
                          "is set. In order to take effect both should be set.")
-    if getattr(params, 'fov_expansion_kernel_size', 0):
-        raise NotImplementedError('increase_fov conv is not built by the native path')
     if getattr(params, 'upsampling_method', 'bilinear') != 'bilinear':
         raise NotImplementedError("only upsampling_method='bilinear' (the default) is fused")
     if getattr(params, 'norm_layer', 'batch') != 'batch':
@@ -70,7 +68,8 @@ def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
     key = (dev, depth, pyramid, params.height_feature_extractor, params.width_feature_extractor,
            nb_pp, nb_pb, nb_pi, getattr(params, 'compute_dtype', 'fp32'),
            params.per_pixel_dataset_name, bool(getattr(params, 'cross_replica_norm', False)),
-           getattr(params, 'ema_decay', 0) > 0)
+           getattr(params, 'ema_decay', 0) > 0,
+           getattr(params, 'fov_expansion_kernel_size', 0), getattr(params, 'fov_expansion_kernel_rate', 0))
     ctx = _CONTEXTS.get(key)
     if ctx is None:
         ctx = SegContext(depth=depth, pyramid=pyramid, height=params.height_feature_extractor,
@@ -81,7 +80,10 @@ def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
                          bn_decay=getattr(params, 'batch_norm_decay', 0.9),
                          train_bn=getattr(params, 'norm_train_variables', True),
                          weight_decay=getattr(params, 'regularization_weight', 0.00017),
-                         ema=getattr(params, 'ema_decay', 0) > 0, device=dev)
+                         ema=getattr(params, 'ema_decay', 0) > 0, device=dev,
+                         # extension/increase_fov (resnet50_extended_feature_extractor.py:44-49)
+                         fov_k=getattr(params, 'fov_expansion_kernel_size', 0),
+                         fov_rate=getattr(params, 'fov_expansion_kernel_rate', 0))
         ctx.load_params(init_params(ctx.param_info, seed=getattr(params, 'init_seed', 0)))
         if getattr(params, 'cross_replica_norm', False):
             # hierarchical.py:327-328: BN statistics over all replicas (torch.distributed)

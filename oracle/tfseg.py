@@ -55,6 +55,8 @@ class SegConfig:
     feature_dims_decreased: int = 256
     bn_decay: float = 0.9            # batch_norm_decay (:269)
     weight_decay: float = 0.00017    # regularization_weight (utils/utils.py:111)
+    fov_k: int = 0                   # fov_expansion_kernel_size (hierarchical.py:247-250)
+    fov_rate: int = 0                # fov_expansion_kernel_rate
 
     @property
     def nb(self) -> int:
@@ -138,6 +140,10 @@ def build_specs(cfg: SegConfig) -> List[ConvSpec]:
         specs += _bottleneck_specs(f"{rn}/{scope}", din, d, dbn, s, r)
     fd = cfg.feature_dims_decreased
     specs.append(ConvSpec("feature_extractor/extension/decrease_fdims", 2048, fd, 1))
+    if cfg.fov_k > 0 and cfg.fov_rate > 0:
+        # resnet50_extended_feature_extractor.py:44-49: slim.conv2d (SAME, BN, ReLU), fd -> fd
+        specs.append(ConvSpec("feature_extractor/extension/increase_fov", fd, fd, cfg.fov_k, 1,
+                              cfg.fov_rate))
     if cfg.pyramid == "psp":
         for i in range(4):
             specs.append(ConvSpec(f"feature_extractor/pyramid_module/Conv{'' if i == 0 else '_%d' % i}",
@@ -486,6 +492,8 @@ class OracleNet:
         for (scope, din, d, dbn, s, r) in resnet_units(cfg.depth, cfg.output_stride):
             x = self.bottleneck(x, f"{rn}/{scope}", s, r, d, record=record)
         x = self.conv_bn(x, "feature_extractor/extension/decrease_fdims", record=record)
+        if cfg.fov_k > 0 and cfg.fov_rate > 0:
+            x = self.conv_bn(x, "feature_extractor/extension/increase_fov", record=record)
         if cfg.pyramid == "psp":
             x = self.psp(x, record=record)
         elif cfg.pyramid == "aspp":

@@ -37,7 +37,8 @@ def _native_step(cuda, cfg, params, data, dtype, lr=0.01, steps=1):
     from seg_hip import SegContext
     ctx = SegContext(depth=cfg.depth, pyramid=cfg.pyramid, height=cfg.height, width=cfg.width,
                      nb_pp=cfg.nb_pp, nb_pb=cfg.nb_pb, nb_pi=cfg.nb_pi, dtype=dtype,
-                     weight_decay=cfg.weight_decay, bn_decay=cfg.bn_decay)
+                     weight_decay=cfg.weight_decay, bn_decay=cfg.bn_decay,
+                     fov_k=cfg.fov_k, fov_rate=cfg.fov_rate)
     ctx.load_params(params)
     img = torch.as_tensor(data["images"]).to(cuda)
     px = torch.as_tensor(data["px"]).to(cuda) if cfg.nb_pp else None
@@ -75,10 +76,12 @@ CONFIGS = [
     SegConfig(height=48, width=64, nb_pp=1, pyramid="none"),
     SegConfig(depth=101, height=48, width=64, nb_pp=1, nb_pb=1, pyramid="psp"),
     SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp"),
+    # extension/increase_fov (resnet50_extended_feature_extractor.py:44-49), 3x3 rate 2
+    SegConfig(height=48, width=64, nb_pp=2, pyramid="psp", fov_k=3, fov_rate=2),
 ]
 
 
-@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"r{c.depth}-{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}")
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"r{c.depth}-{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}" + (f"-fov{c.fov_k}r{c.fov_rate}" if c.fov_k else ""))
 def test_train_step_fp32(cuda, cfg):
     from input_pipelines.synthetic import batch
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=3).items()}
@@ -141,12 +144,14 @@ def test_train_step_fp32(cuda, cfg):
 # (pyramid, depth, dtype, strong : bbox : tag) -- R101 with the C4 (bf16) and C5 (fp16) mixes
 LAYERWISE = [("psp", 50, "bf16", (1, 1, 0)), ("aspp", 50, "bf16", (1, 1, 0)),
              ("psp", 50, "fp16", (1, 1, 0)), ("aspp", 50, "fp16", (1, 1, 0)),
-             ("aspp", 101, "bf16", (2, 2, 0)), ("aspp", 101, "fp16", (1, 2, 1))]
+             ("aspp", 101, "bf16", (2, 2, 0)), ("aspp", 101, "fp16", (1, 2, 1)),
+             ("aspp", 50, "bf16", (2, 0, 0), (5, 3))]   # + increase_fov 5x5 rate 3
 
 
-@pytest.mark.parametrize("pyramid,depth,dtype,mix", LAYERWISE,
-                         ids=[f"{p}-r{d}-{t}-{''.join(map(str, m))}" for p, d, t, m in LAYERWISE])
-def test_bf16_layerwise(cuda, pyramid, depth, dtype, mix):
+@pytest.mark.parametrize("pyramid,depth,dtype,mix,fov", [t if len(t) == 5 else t + ((0, 0),) for t in LAYERWISE],
+                         ids=[f"{t[0]}-r{t[1]}-{t[2]}-{''.join(map(str, t[3]))}" + (f"-fov{t[4][0]}r{t[4][1]}" if len(t) == 5 else "")
+                              for t in LAYERWISE])
+def test_bf16_layerwise(cuda, pyramid, depth, dtype, mix, fov):
     """16-bit storage / fp32 accumulation, layer by layer.
 
     End-to-end bf16-vs-fp64 comparison is meaningless at random init: the network is chaotic
@@ -157,11 +162,12 @@ def test_bf16_layerwise(cuda, pyramid, depth, dtype, mix):
     from oracle.tfseg import build_specs, conv_tf
     from seg_hip import SegContext
     npp, npb, npi = mix
-    cfg = SegConfig(depth=depth, height=64, width=128, nb_pp=npp, nb_pb=npb, nb_pi=npi, pyramid=pyramid)
+    cfg = SegConfig(depth=depth, height=64, width=128, nb_pp=npp, nb_pb=npb, nb_pi=npi, pyramid=pyramid,
+                    fov_k=fov[0], fov_rate=fov[1])
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=5).items()}
     data = batch(12, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
     ctx = SegContext(depth=depth, pyramid=pyramid, height=64, width=128, nb_pp=npp, nb_pb=npb,
-                     nb_pi=npi, dtype=dtype)
+                     nb_pi=npi, dtype=dtype, fov_k=fov[0], fov_rate=fov[1])
     ctx.load_params(params)
     dev = lambda a: None if a is None else torch.as_tensor(a).to(cuda)
     ctx.forward(torch.as_tensor(data["images"]).to(cuda))

@@ -260,3 +260,22 @@ def test_conv_props_match_conv_tf_and_autograd(case):
     torch.testing.assert_close(conv_dgrad(dyn, w, spec, H, W), xt.grad.permute(0, 2, 3, 1),
                                rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(conv_wgrad(x, dyn, spec), wt.grad, rtol=1e-12, atol=1e-12)
+
+
+def test_increase_fov_spec_order_and_validation():
+    """extension/increase_fov (resnet50_extended_feature_extractor.py:44-49) follows
+    decrease_fdims in variable-creation order, fd -> fd channels, SAME, BN + ReLU; setting only
+    one of the two flags is an error (hierarchical.py:272-274)."""
+    import argparse
+    from oracle.tfseg import build_specs
+    from models.resnet50_extended_model_hierarchical import _validate_params
+    specs = build_specs(SegConfig(pyramid="psp", fov_k=3, fov_rate=2))
+    names = [s.name for s in specs]
+    i = names.index("feature_extractor/extension/increase_fov")
+    assert names[i - 1] == "feature_extractor/extension/decrease_fdims"
+    s = specs[i]
+    assert (s.ci, s.co, s.k, s.stride, s.rate, s.relu, s.explicit_pad) == (256, 256, 3, 1, 2, True, False)
+    assert "feature_extractor/extension/increase_fov" not in [x.name for x in build_specs(SegConfig())]
+    with pytest.raises(ValueError):
+        _validate_params(argparse.Namespace(fov_expansion_kernel_size=3, fov_expansion_kernel_rate=0))
+    _validate_params(argparse.Namespace(fov_expansion_kernel_size=3, fov_expansion_kernel_rate=2))
