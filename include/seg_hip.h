@@ -43,7 +43,8 @@ enum { SEG_PYRAMID_NONE = 0, SEG_PYRAMID_PSP = 1, SEG_PYRAMID_ASPP = 2 };
 enum { SEG_DTYPE_F32 = 0, SEG_DTYPE_BF16 = 1, SEG_DTYPE_F16 = 2 };
 enum { SEG_DATASET_CITYSCAPES = 0, SEG_DATASET_VISTAS = 1 };
 enum { SEG_PARAM_WEIGHTS = 0, SEG_PARAM_GAMMA = 1, SEG_PARAM_BETA = 2,
-       SEG_PARAM_MOVING_MEAN = 3, SEG_PARAM_MOVING_VAR = 4 };
+       SEG_PARAM_MOVING_MEAN = 3, SEG_PARAM_MOVING_VAR = 4, SEG_PARAM_BIASES = 5 };
+enum { SEG_UPSAMPLING_BILINEAR = 0, SEG_UPSAMPLING_HYBRID = 1 };
 
 typedef struct seg_cfg {
   int depth;            /* 50 | 101 (name_feature_extractor) */
@@ -59,6 +60,8 @@ typedef struct seg_cfg {
   float weight_decay;   /* regularization_weight (0.00017): l2_regularizer scale */
   int fov_k, fov_rate;  /* fov_expansion_kernel_size / _rate: the optional extension/increase_fov
                            conv (resnet50_extended_feature_extractor.py:44-49); 0 = off */
+  int upsampling;       /* SEG_UPSAMPLING_* (upsampling_method, hierarchical.py:143-184): hybrid
+                           adds a 3x3 conv2d_transpose + bias per logits head before the resize */
 } seg_cfg;
 
 /* lifecycle -------------------------------------------------------------------------- */
@@ -79,7 +82,9 @@ int seg_bind_buffers(seg_ctx* ctx, float* params, float* grads, float* momentum,
 int64_t seg_param_count(seg_ctx* ctx);
 int seg_param_info(seg_ctx* ctx, int64_t i, const char** name, int64_t* offset,
                    int64_t* numel, int* kind);
-/* dims[4]: weights (Co, KH, KW, Ci); BN vectors (C, 1, 1, 1) */
+/* dims[4]: weights (Co, KH, KW, Ci); BN vectors and biases (C, 1, 1, 1). The hybrid
+ * upsampler's conv2d_transpose weights are (Cin, 3, 3, Cout) so that the OHWI -> HWIO export
+ * gives TF's [h][w][out][in] filter layout */
 int seg_param_shape(seg_ctx* ctx, int64_t i, int64_t* dims);
 /* re-derive compute copies (bf16 weights, flipped dgrad weights) after a host write */
 int seg_params_updated(seg_ctx* ctx, void* stream);

@@ -16,6 +16,7 @@
 #include "bn.h"
 #include "input.h"
 #include "conv.h"
+#include "deconv.h"
 #include "loss.h"
 #include "labels.h"
 #include "optim.h"
@@ -142,7 +143,14 @@ struct seg_ctx {
   Unit heads[3];
   int logit_conv[3] = {-1, -1, -1};
   Act logits;                     // fp32 [N][Hl][Wl][ldl]
-  float* grad_un = nullptr;       // fp32 same shape
+  float* grad_un = nullptr;       // fp32 same shape (gradient w.r.t. head_in)
+  // 'hybrid' upsampling: per-head 3x3 conv2d_transpose + bias on the logits (deconv.h)
+  bool hybrid = false;
+  long dc_w_off[3] = {0, 0, 0}, dc_b_off[3] = {0, 0, 0}, dc_b_lo = 0;
+  float* up_in = nullptr;         // deconv output [N][Hl][Wl][ldl]
+  float* dc_dx = nullptr;         // gradient w.r.t. the logits [N][Hl][Wl][ldl]
+  float* dc_part = nullptr;       // weight-gradient tile partials
+  const float* head_in = nullptr; // what the bilinear upsampler reads: logits or up_in
   int ldl = 0, nc[3] = {0, 0, 0};
   LossTables tables{};
   float* loss_part = nullptr;
@@ -768,11 +776,21 @@ int build(seg_ctx* c) {
     c->logit_conv[h] = add_conv(c, std::string("softmax_classifier/") + hn[h] + "_logits", fd, c->nc[h], 1, 1, 1, false, false);
   c->convs[c->stem].need_dgrad = false;
 
+  if (g.upsampling != SEG_UPSAMPLING_BILINEAR && g.upsampling != SEG_UPSAMPLING_HYBRID)
+    return set_err(&c->err, -EINVAL, "upsampling must be bilinear or hybrid");
+  c->hybrid = g.upsampling == SEG_UPSAMPLING_HYBRID;
+
   // ---- flat parameter layout ----
+  // [conv weights | hybrid deconv weights] (weight decay) [BN gamma/beta | deconv biases]
   long off = 0;
   for (auto& L : c->convs) { L.w_off = off; off += (long)L.co * L.k * L.k * L.ci; }
+  if (c->hybrid)
+    for (int h = 0; h < 3; ++h) { c->dc_w_off[h] = off; off += 9L * c->nc[h] * c->nc[h]; }
   c->n_decay = off;
   for (auto& L : c->convs) { L.g_off = off; off += L.co; L.b_off = off; off += L.co; }
+  c->dc_b_lo = off;
+  if (c->hybrid)
+    for (int h = 0; h < 3; ++h) { c->dc_b_off[h] = off; off += c->nc[h]; }
   c->n_train = off;
   long moff = 0;
   for (auto& L : c->convs) { L.mv_off = moff; moff += L.co; }
@@ -811,6 +829,17 @@ int build(seg_ctx* c) {
     c->pinfo.push_back({L.name + "/BatchNorm/gamma", L.g_off, L.co, SEG_PARAM_GAMMA, {L.co, 1, 1, 1}});
     c->pinfo.push_back({L.name + "/BatchNorm/moving_mean", L.mv_off, L.co, SEG_PARAM_MOVING_MEAN, {L.co, 1, 1, 1}});
     c->pinfo.push_back({L.name + "/BatchNorm/moving_variance", moff + L.mv_off, L.co, SEG_PARAM_MOVING_VAR, {L.co, 1, 1, 1}});
+  }
+  if (c->hybrid) {
+    // slim.conv2d_transpose default scopes inside softmax_classifier/upsampling, created after
+    // the three logits convs (hierarchical.py:84-86,168-180)
+    const char* sfx[3] = {"", "_1", "_2"};
+    for (int h = 0; h < 3; ++h) {
+      const std::string nm = std::string("softmax_classifier/upsampling/Conv2d_transpose") + sfx[h];
+      const int C = c->nc[h];
+      c->pinfo.push_back({nm + "/weights", c->dc_w_off[h], 9L * C * C, SEG_PARAM_WEIGHTS, {C, 3, 3, C}});
+      c->pinfo.push_back({nm + "/biases", c->dc_b_off[h], C, SEG_PARAM_BIASES, {C, 1, 1, 1}});
+    }
   }
 
   // ---- activations ----
@@ -914,6 +943,14 @@ int build(seg_ctx* c) {
   c->ldl = ((c->nc[0] + c->nc[1] + c->nc[2] + 3) / 4) * 4;
   if (int r = alloc_act(c, c->logits, N, Hf, Wf, c->nc[0] + c->nc[1] + c->nc[2], c->ldl, 4)) return r;
   if (int r = dalloc(c, &c->grad_un, (size_t)N * Hf * Wf * c->ldl)) return r;
+  c->head_in = (const float*)c->logits.p;
+  if (c->hybrid) {
+    if (int r = dalloc(c, &c->up_in, (size_t)N * Hf * Wf * c->ldl)) return r;
+    if (int r = dalloc(c, &c->dc_dx, (size_t)N * Hf * Wf * c->ldl)) return r;
+    const size_t np = (size_t)deconv_wgrad_blocks(N, Hf, Wf, c->nc[0] + c->nc[1] + c->nc[2]) * deconv_nw(c->nc);
+    if (int r = dalloc(c, &c->dc_part, np)) return r;
+    c->head_in = c->up_in;
+  }
   c->loss_blocks = loss_head_blocks(N, Hf, Wf);
   if (int r = dalloc(c, &c->loss_part, (size_t)c->loss_blocks * 8)) return r;
   if (int r = dalloc(c, &c->loss_out, 16)) return r;
@@ -1000,6 +1037,19 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
   return 0;
 }
 
+DeconvArgs deconv_args(seg_ctx* c) {
+  DeconvArgs a{};
+  a.x = (const float*)c->logits.p; a.y = c->up_in; a.g = c->grad_un; a.gscale = c->dzscale;
+  a.dx = c->dc_dx; a.part = c->dc_part;
+  a.N = c->logits.N; a.H = c->logits.H; a.W = c->logits.W; a.ld = c->ldl;
+  for (int h = 0; h < 3; ++h) {
+    a.c[h] = c->nc[h];
+    a.w[h] = c->params + c->dc_w_off[h]; a.b[h] = c->params + c->dc_b_off[h];
+    a.gw[h] = c->grads + c->dc_w_off[h]; a.gb[h] = c->grads + c->dc_b_off[h];
+  }
+  return a;
+}
+
 Act logits_slice(seg_ctx* c, int h) {
   int off = 0;
   for (int i = 0; i < h; ++i) off += c->nc[i];
@@ -1079,6 +1129,7 @@ int forward(Step& S, const float* images) {
     if (int r = conv_forward(S, c->logit_conv[h], c->heads[h].out)) return r;
     if (int r = bn_apply(S, c->logit_conv[h], logits_slice(c, h), 1)) return r;
   }
+  if (c->hybrid) HIPCALL(c, launch_deconv_fwd(deconv_args(c), S.s));
   return 0;
 }
 
@@ -1106,11 +1157,15 @@ int backward(Step& S) {
 
 int backward_layers(Step& S) {
   seg_ctx* c = S.c;
+  // hybrid: the loss-normalised gradient goes back through the deconvolution first (its
+  // weight / bias gradients and dx), then into the logits BN without a further scale
+  if (c->hybrid) HIPCALL(c, launch_deconv_bwd(deconv_args(c), S.s));
   for (int h = 0; h < 3; ++h) {
     Act gz = logits_slice(c, h);
     int off = (int)((float*)gz.p - (float*)c->logits.p);
-    gz.p = c->grad_un + off;
-    if (int r = bn_backward(S, c->logit_conv[h], gz, 1, nullptr, nullptr, c->dzscale + off)) return r;
+    gz.p = (c->hybrid ? c->dc_dx : c->grad_un) + off;
+    if (int r = bn_backward(S, c->logit_conv[h], gz, 1, nullptr, nullptr,
+                            c->hybrid ? nullptr : c->dzscale + off)) return r;
     if (int r = conv_wgrad(S, c->logit_conv[h], c->heads[h].out)) return r;
     if (int r = conv_dgrad(S, c->logit_conv[h], c->heads[h].dout)) return r;
     if (int r = unit_backward(S, c->heads[h], c->dfeat, h > 0)) return r;
@@ -1326,7 +1381,7 @@ int seg_loss(seg_ctx* c, const int32_t* px, const float* bbox, const float* tag,
   if ((g.nb_pp && !px) || (g.nb_pb && !bbox) || (g.nb_pi && !tag))
     return set_err(&c->err, -EINVAL, "missing labels for a non-empty sub-batch");
   LossArgs a{};
-  a.logits = (const float*)c->logits.p; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
+  a.logits = c->head_in; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
   a.ldl = c->ldl; a.H = g.height; a.W = g.width;
   a.npp = g.nb_pp; a.npb = g.nb_pb; a.npi = g.nb_pi;
   a.px_labels = px; a.bbox_soft = bbox; a.tag_soft = tag;
@@ -1367,7 +1422,7 @@ int seg_predict(seg_ctx* c, const int32_t* cid_map, int n_map, int replace_voids
                    n_map, c->tables.n_pp);
   if (out_h < 1 || out_w < 1) return set_err(&c->err, -EINVAL, "bad output size %dx%d", out_h, out_w);
   EvalArgs a{};
-  a.logits = (const float*)c->logits.p; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
+  a.logits = c->head_in; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
   a.ldl = c->ldl; a.H = g.height; a.W = g.width; a.Ho = out_h; a.Wo = out_w;
   a.replace_voids = replace_voids ? 1 : 0; a.n_map = n_map; a.out = decisions_out;
   int mx = -1;
@@ -1384,7 +1439,7 @@ int seg_full_predictions(seg_ctx* c, float* logits_out, float* probs_out,
                          int32_t* head_decisions_out, int32_t* decisions_out, void* stream) {
   NEED_BOUND(c);
   FullPredArgs a{};
-  a.logits = (const float*)c->logits.p; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
+  a.logits = c->head_in; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
   a.ldl = c->ldl; a.H = c->cfg.height; a.W = c->cfg.width;
   a.logits_out = logits_out; a.probs_out = probs_out;
   a.head_decs_out = head_decisions_out; a.decs_out = decisions_out;
@@ -1427,6 +1482,12 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
     b.ema = a.ema ? c->ema + c->n_decay : nullptr; b.w_lp = nullptr; b.n = c->n_train - c->n_decay;
     b.wd = 0.f; b.reg_part = nullptr;
     HIPCALL(c, launch_sgdm(b, s));
+  } else if (c->hybrid) {   // frozen BN parameters: the deconv biases still train
+    SgdmArgs b = a;
+    b.w = c->params + c->dc_b_lo; b.g = c->grads + c->dc_b_lo; b.v = c->mom + c->dc_b_lo;
+    b.ema = a.ema ? c->ema + c->dc_b_lo : nullptr; b.w_lp = nullptr; b.n = c->n_train - c->dc_b_lo;
+    b.wd = 0.f; b.reg_part = nullptr;
+    HIPCALL(c, launch_sgdm(b, s));
   }
   const long half = c->n_moving / 2;
   HIPCALL(c, launch_moving_update(c->moving, c->moving + half, c->grads + c->n_train,
@@ -1440,7 +1501,7 @@ int seg_outputs(seg_ctx* c, const float** losses, const float** reg, const float
   if (!c) return set_err(nullptr, -EINVAL, "null ctx");
   if (losses) *losses = c->loss_out;
   if (reg) *reg = c->reg_out;
-  if (logits) *logits = (const float*)c->logits.p;
+  if (logits) *logits = c->head_in;
   if (ld) *ld = c->ldl;
   if (hl) *hl = c->logits.H;
   if (wl) *wl = c->logits.W;
@@ -1563,6 +1624,7 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
   Act a;
   int dt = c->dt == SEG_BF16 ? SEG_DTYPE_BF16 : (c->dt == SEG_F16 ? SEG_DTYPE_F16 : SEG_DTYPE_F32);
   if (n == "logits") { a = c->logits; dt = SEG_DTYPE_F32; }
+  else if (n == "head_in") { a = c->logits; a.p = (void*)c->head_in; dt = SEG_DTYPE_F32; }
   else if (n == "grad_un") { a = c->logits; a.p = c->grad_un; dt = SEG_DTYPE_F32; }
   else if (n == "dzscale") { a.p = c->dzscale; a.N = a.H = a.W = 1; a.C = a.ld = c->ldl; dt = SEG_DTYPE_F32; }
   else if (n == "feat") a = c->feat;

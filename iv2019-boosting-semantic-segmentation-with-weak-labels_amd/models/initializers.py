@@ -1,8 +1,9 @@
 """Seeded parameter initialisation with the reference's initializer semantics.
 
 Conv weights: ``slim.variance_scaling_initializer()`` (factor 2.0, FAN_IN, truncated normal
-with stddev sqrt(1.3 * 2 / fan_in)) — the arg scope at hierarchical.py:336-339. BN: gamma 1,
-beta 0, moving mean 0, moving variance 1. The ImageNet warm start
+with stddev sqrt(1.3 * 2 / fan_in)) — the arg scope at hierarchical.py:336-339; the hybrid
+upsampler's conv2d_transpose weights the same (hierarchical.py:174-175; fan_in = 9 C, stored
+(Cin, 3, 3, Cout)), its biases 0. BN: gamma 1, beta 0, moving mean 0, moving variance 1. The ImageNet warm start
 (define_initializers.py:72-131) needs a checkpoint that is not available.
 
 Seeding scheme (documented so any implementation reproduces it): the i-th conv in

@@ -37,8 +37,10 @@ def _validate_params(params):
             getattr(params, 'fov_expansion_kernel_size', 0)):
         raise ValueError("One of params.{fov_expansion_kernel_rate, fov_expansion_kernel_size} "
                          "is set. In order to take effect both should be set.")
-    if getattr(params, 'upsampling_method', 'bilinear') != 'bilinear':
-        raise NotImplementedError("only upsampling_method='bilinear' (the default) is fused")
+    if getattr(params, 'upsampling_method', 'bilinear') not in ('bilinear', 'hybrid'):
+        # 'no' leaves the logits at H/8 x W/8, which the reference's own losses cannot
+        # compare with full-resolution labels
+        raise NotImplementedError("upsampling_method must be 'bilinear' (default) or 'hybrid'")
     if getattr(params, 'norm_layer', 'batch') != 'batch':
         raise NotImplementedError("only norm_layer='batch' is implemented")
     if getattr(params, 'stride_feature_extractor', 8) != 8:
@@ -69,7 +71,8 @@ def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
            nb_pp, nb_pb, nb_pi, getattr(params, 'compute_dtype', 'fp32'),
            params.per_pixel_dataset_name, bool(getattr(params, 'cross_replica_norm', False)),
            getattr(params, 'ema_decay', 0) > 0,
-           getattr(params, 'fov_expansion_kernel_size', 0), getattr(params, 'fov_expansion_kernel_rate', 0))
+           getattr(params, 'fov_expansion_kernel_size', 0), getattr(params, 'fov_expansion_kernel_rate', 0),
+           getattr(params, 'upsampling_method', 'bilinear'))
     ctx = _CONTEXTS.get(key)
     if ctx is None:
         ctx = SegContext(depth=depth, pyramid=pyramid, height=params.height_feature_extractor,
@@ -83,7 +86,9 @@ def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
                          ema=getattr(params, 'ema_decay', 0) > 0, device=dev,
                          # extension/increase_fov (resnet50_extended_feature_extractor.py:44-49)
                          fov_k=getattr(params, 'fov_expansion_kernel_size', 0),
-                         fov_rate=getattr(params, 'fov_expansion_kernel_rate', 0))
+                         fov_rate=getattr(params, 'fov_expansion_kernel_rate', 0),
+                         # 'hybrid': conv2d_transpose + bias per head (hierarchical.py:168-180)
+                         upsampling=getattr(params, 'upsampling_method', 'bilinear'))
         ctx.load_params(init_params(ctx.param_info, seed=getattr(params, 'init_seed', 0)))
         if getattr(params, 'cross_replica_norm', False):
             # hierarchical.py:327-328: BN statistics over all replicas (torch.distributed)

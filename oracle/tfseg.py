@@ -57,6 +57,7 @@ class SegConfig:
     weight_decay: float = 0.00017    # regularization_weight (utils/utils.py:111)
     fov_k: int = 0                   # fov_expansion_kernel_size (hierarchical.py:247-250)
     fov_rate: int = 0                # fov_expansion_kernel_rate
+    upsampling: str = "bilinear"     # upsampling_method (hierarchical.py:143-184): bilinear | hybrid
 
     @property
     def nb(self) -> int:
@@ -196,7 +197,20 @@ def init_params(cfg: SegConfig, seed: int = 0) -> Dict[str, np.ndarray]:
         p[f"{s.name}/BatchNorm/beta"] = np.zeros(s.co)
         p[f"{s.name}/BatchNorm/moving_mean"] = np.zeros(s.co)
         p[f"{s.name}/BatchNorm/moving_variance"] = np.ones(s.co)
+    if cfg.upsampling == "hybrid":
+        n0 = len(build_specs(cfg))
+        for h, c in enumerate(n_classes(cfg.dataset)):
+            rng = np.random.default_rng([seed, n0 + h])
+            name = deconv_scope(h)
+            p[f"{name}/weights"] = truncated_normal(rng, (c, 3, 3, c), math.sqrt(1.3 * 2.0 / (9 * c)))
+            p[f"{name}/biases"] = np.zeros(c)
     return p
+
+
+def deconv_scope(h: int) -> str:
+    """slim.conv2d_transpose default scope of head h's hybrid upsampler (hierarchical.py:168-180):
+    created after the three logits convs inside softmax_classifier/upsampling."""
+    return "softmax_classifier/upsampling/Conv2d_transpose" + ("", "_1", "_2")[h]
 
 
 # ----------------------------------------------------------------------------------------
@@ -500,11 +514,18 @@ class OracleNet:
             x = self.aspp(x, record=record)
         feats = x
         heads = {}
-        for head in ("l1", "l2_vehicle", "l2_human"):
+        for h, head in enumerate(("l1", "l2_vehicle", "l2_human")):
             f = self.bottleneck(x, f"adaptation_module/{head}_features", 1, 1, x.shape[1],
                                 record=record)
             heads[head] = self.conv_bn(f, f"softmax_classifier/{head}_logits", relu=False,
                                        record=record)
+            if cfg.upsampling == "hybrid":
+                # slim.conv2d_transpose(C, 3, SAME, stride 1, activation None, bias) before the
+                # resize (hierarchical.py:168-180); TF filter [kh][kw][out][in] is stored
+                # D[in][kh][kw][out], i.e. torch's conv_transpose2d weight [in][out][kh][kw]
+                sc = deconv_scope(h)
+                heads[head] = F.conv_transpose2d(heads[head], self.p[f"{sc}/weights"].permute(0, 3, 1, 2),
+                                                 self.p[f"{sc}/biases"], padding=1)
         return {"features": feats, "l1_logits": heads["l1"],
                 "l2_vehicle_logits": heads["l2_vehicle"], "l2_human_logits": heads["l2_human"]}
 

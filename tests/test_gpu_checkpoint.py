@@ -17,11 +17,13 @@ def _ctx(**kw):
     return SegContext(**a)
 
 
-def test_export_import_round_trip(cuda, tmp_path):
+@pytest.mark.parametrize("upsampling", ["bilinear", "hybrid"])
+def test_export_import_round_trip(cuda, tmp_path, upsampling):
     from models.initializers import init_params
     from utils.tf_checkpoint import export_checkpoint, import_checkpoint, list_variables
-    a = _ctx()
+    a = _ctx(upsampling=upsampling)
     a.load_params(init_params(a.param_info, seed=7))
+    a.params.normal_()   # non-zero biases too
     a.moving.uniform_(0.5, 1.5)
     a.momentum.normal_()
     pre = str(tmp_path / "model.ckpt-42")
@@ -30,7 +32,14 @@ def test_export_import_round_trip(cuda, tmp_path):
     w = [p for p in a.param_info if p.kind == "weights"][0]
     assert names[w.name] == [w.shape[1], w.shape[2], w.shape[3], w.shape[0]]   # HWIO
     assert w.name + "/Momentum" in names and "global_step" in names
-    b = _ctx()
+    if upsampling == "hybrid":   # conv2d_transpose filters [kh][kw][out][in] + biases [C]
+        from utils.tf_checkpoint import load_checkpoint
+        sc = "softmax_classifier/upsampling/Conv2d_transpose_1"
+        assert names[sc + "/weights"] == [3, 3, 7, 7] and names[sc + "/biases"] == [7]
+        d = a.named("params")[sc + "/weights"].reshape(7, 3, 3, 7)   # [in][kh][kw][out]
+        tf_w = load_checkpoint(pre, [sc + "/weights"])[sc + "/weights"]
+        assert np.array_equal(tf_w, d.transpose(1, 2, 3, 0))
+    b = _ctx(upsampling=upsampling)
     assert import_checkpoint(b, pre) == 42
     torch.cuda.synchronize()
     assert torch.equal(a.params, b.params) and torch.equal(a.moving, b.moving)

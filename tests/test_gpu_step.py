@@ -38,7 +38,7 @@ def _native_step(cuda, cfg, params, data, dtype, lr=0.01, steps=1):
     ctx = SegContext(depth=cfg.depth, pyramid=cfg.pyramid, height=cfg.height, width=cfg.width,
                      nb_pp=cfg.nb_pp, nb_pb=cfg.nb_pb, nb_pi=cfg.nb_pi, dtype=dtype,
                      weight_decay=cfg.weight_decay, bn_decay=cfg.bn_decay,
-                     fov_k=cfg.fov_k, fov_rate=cfg.fov_rate)
+                     fov_k=cfg.fov_k, fov_rate=cfg.fov_rate, upsampling=cfg.upsampling)
     ctx.load_params(params)
     img = torch.as_tensor(data["images"]).to(cuda)
     px = torch.as_tensor(data["px"]).to(cuda) if cfg.nb_pp else None
@@ -78,10 +78,12 @@ CONFIGS = [
     SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp"),
     # extension/increase_fov (resnet50_extended_feature_extractor.py:44-49), 3x3 rate 2
     SegConfig(height=48, width=64, nb_pp=2, pyramid="psp", fov_k=3, fov_rate=2),
+    # upsampling_method='hybrid' (hierarchical.py:168-180): 3x3 conv2d_transpose + bias per head
+    SegConfig(height=48, width=64, nb_pp=1, nb_pb=1, pyramid="none", upsampling="hybrid"),
 ]
 
 
-@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"r{c.depth}-{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}" + (f"-fov{c.fov_k}r{c.fov_rate}" if c.fov_k else ""))
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"r{c.depth}-{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}" + (f"-fov{c.fov_k}r{c.fov_rate}" if c.fov_k else "") + ("-hybrid" if c.upsampling == "hybrid" else ""))
 def test_train_step_fp32(cuda, cfg):
     from input_pipelines.synthetic import batch
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=3).items()}

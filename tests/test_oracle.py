@@ -279,3 +279,33 @@ def test_increase_fov_spec_order_and_validation():
     with pytest.raises(ValueError):
         _validate_params(argparse.Namespace(fov_expansion_kernel_size=3, fov_expansion_kernel_rate=0))
     _validate_params(argparse.Namespace(fov_expansion_kernel_size=3, fov_expansion_kernel_rate=2))
+
+
+def test_hybrid_deconv_matches_tf_conv2d_transpose_definition():
+    """The oracle's hybrid upsampler (F.conv_transpose2d on D[in][kh][kw][out]) equals TF's
+    conv2d_transpose definition written out: y[p][o] = b[o] + sum_{kh,kw,i}
+    x[p + 1 - (kh, kw)][i] * W[kh][kw][o][i] (SAME, stride 1, zero outside the map)."""
+    rng = np.random.default_rng(3)
+    c, h, w = 5, 6, 7
+    x = rng.standard_normal((1, c, h, w))
+    W = rng.standard_normal((3, 3, c, c))            # TF filter [kh][kw][out][in]
+    b = rng.standard_normal(c)
+    D = W.transpose(3, 0, 1, 2)                      # [in][kh][kw][out]
+    got = F.conv_transpose2d(torch.tensor(x), torch.tensor(D).permute(0, 3, 1, 2),
+                             torch.tensor(b), padding=1).numpy()
+    ref = np.tile(b[None, :, None, None], (1, 1, h, w))
+    for py in range(h):
+        for px in range(w):
+            for kh in range(3):
+                for kw in range(3):
+                    qy, qx = py + 1 - kh, px + 1 - kw
+                    if 0 <= qy < h and 0 <= qx < w:
+                        ref[0, :, py, px] += W[kh, kw] @ x[0, :, qy, qx]
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
+    cfg = SegConfig(height=64, width=128, pyramid="none", upsampling="hybrid")
+    p = tfseg.init_params(cfg, seed=1)
+    assert p["softmax_classifier/upsampling/Conv2d_transpose_2/weights"].shape == (3, 3, 3, 3)
+    assert np.all(p["softmax_classifier/upsampling/Conv2d_transpose/biases"] == 0)
+    net = OracleNet(cfg, p)
+    low = net.forward(torch.zeros(1, 64, 128, 3, dtype=torch.float64))
+    assert low["l1_logits"].shape == (1, 14, 8, 16)
