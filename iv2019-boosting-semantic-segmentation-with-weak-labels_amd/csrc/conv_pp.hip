@@ -54,19 +54,13 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// one butterfly step of per-channel (sum, M2) pairs between DPP partner lanes, equal counts n
-// (scalar: a DPP move feeding packed fp32 math miscompiled for lanes 1-3 of the vector)
+// v[r] += v[r] of the DPP partner lane. Scalar: a DPP move feeding packed fp32 math
+// miscompiled for lanes 1-3 of the vector
 template <int CTRL>
-__device__ __forceinline__ void chan_step(float (&sm)[4], float (&m2)[4], float n) {
-  const float inv = 1.f / n, hn = 0.5f * n;
+__device__ __forceinline__ void row_sum(float (&v)[4]) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float s2 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, sm[r]), CTRL, 0xf, 0xf, false));
-    const float q2 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, m2[r]), CTRL, 0xf, 0xf, false));
-    const float d = (s2 - sm[r]) * inv;
-    m2[r] = m2[r] + q2 + d * d * hn;
-    sm[r] += s2;
-  }
+  for (int r = 0; r < 4; ++r)
+    v[r] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[r]), CTRL, 0xf, 0xf, false));
 }
 
 // PERSIST: loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
@@ -133,6 +127,13 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       // the per-tile setup on short-K layers
       const int m = (int)m0_ + row;
       const bool ok = m < (int)M;
+      if constexpr (ST == 0) {
+        // 1x1, stride 1, no padding (H x W = Ho x Wo): the source row IS pixel m, every tap
+        // valid; no pixel decode (the divisions were ~2.5k cycles of the per-tile setup)
+        a_voff[j] = (ok ? m : 0) * a.ldx * 2 + a_lc[j] * 16;
+        a_bits[j] = ok ? 0x11 : 0;
+        continue;
+      }
       const unsigned mm = ok ? (unsigned)m : 0u;
       const unsigned t = mm / (unsigned)a.Wo;
       const int wo = (int)(mm - t * (unsigned)a.Wo);
@@ -188,7 +189,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       if (hid < 2) {
         const int j = hid * 2 + i;
         uint32_t off;
-        if constexpr (ST == 1) {
+        if constexpr (ST <= 1) {
           off = (a_bits[j] & t.need) == t.need ? (uint32_t)(a_voff[j] + t.s_tap2) : OOB;
         } else {
           int hi = a_h0[j] + t.dh, wi = a_w0[j] + t.dw;
@@ -340,13 +341,19 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         for (int j = 0; j < 2; ++j) {
           float sm[4], m2[4];
           if (full) {
-            // 8 rows in the lane: exact two-pass moments, then a DPP butterfly over the 16
-            // lanes of the row group (pairs via quad_perm xor 1, xor 2, row_half_mirror,
-            // row_mirror), equal counts 8 -> 64: M2 += d^2 * n / 2 with d = (s_b - s_a) / n
+            // exact two-pass moments over the wave row's 128 rows: the 8 rows of the lane are
+            // summed, the sum is completed over the 16 lanes of the row group by a DPP-add
+            // butterfly (quad_perm xor 1, xor 2, row_half_mirror, row_mirror: every lane ends
+            // with the total), then the squared deviations from that mean the same way
             f32x4_t s4 = acc[0][qn][0][j];
 #pragma unroll
             for (int f = 1; f < 8; ++f) s4 += acc[f >> 2][qn][f & 3][j];
-            const f32x4_t mu = s4 * 0.125f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sm[r] = s4[r];
+            row_sum<0xB1>(sm); row_sum<0x4E>(sm); row_sum<0x141>(sm); row_sum<0x140>(sm);
+            f32x4_t mu;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mu[r] = sm[r] * (1.f / 128.f);
             f32x4_t q4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int f = 0; f < 8; ++f) {
@@ -354,14 +361,8 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
               q4 += d * d;
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              sm[r] = s4[r];
-              m2[r] = q4[r];
-            }
-            chan_step<0xB1>(sm, m2, 8.f);
-            chan_step<0x4E>(sm, m2, 16.f);
-            chan_step<0x141>(sm, m2, 32.f);
-            chan_step<0x140>(sm, m2, 64.f);
+            for (int r = 0; r < 4; ++r) m2[r] = q4[r];
+            row_sum<0xB1>(m2); row_sum<0x4E>(m2); row_sum<0x141>(m2); row_sum<0x140>(m2);
           } else {
             // ragged last tile: per-lane counts, general merges
             int c = 0;
@@ -570,6 +571,9 @@ bool conv_nt_pp_ok(const ConvArgs& a) {
 
 template <typename E>
 hipError_t nt_pp_e(const ConvArgs& a, hipStream_t s) {
+  if (a.st == 1 && a.KH == 1 && a.KW == 1 && a.sf == 1 && a.pad_h == 0 && a.pad_w == 0 &&
+      a.H == a.Ho && a.W == a.Wo)
+    return pp_launch_st<E, 0>(a, s);   // dense 1x1 rows
   if (a.st == 1) return pp_launch_st<E, 1>(a, s);
   if (a.st == 2) return pp_launch_st<E, 2>(a, s);
   return hipErrorInvalidValue;
