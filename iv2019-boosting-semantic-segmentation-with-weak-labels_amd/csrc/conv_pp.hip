@@ -54,13 +54,22 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// v[r] += v[r] of the DPP partner lane. Scalar: a DPP move feeding packed fp32 math
-// miscompiled for lanes 1-3 of the vector
-template <int CTRL>
-__device__ __forceinline__ void row_sum(float (&v)[4]) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    v[r] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[r]), CTRL, 0xf, 0xf, false));
+// v[r] += v[r] of the DPP partner lane, as one v_add_f32_dpp per value (the builtin form
+// was a v_mov_b32_dpp + v_add pair). The s_nop covers the VALU-write -> DPP-read hazard of the
+// previous step's results (inline asm is opaque to the hazard recognizer).
+#define PP_ROW_SUM(CTRL)                                                                 \
+  asm volatile("s_nop 1\n"                                                              \
+               "v_add_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n"          \
+               "v_add_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf\n"          \
+               "v_add_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf\n"          \
+               "v_add_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf"             \
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]))
+__device__ __forceinline__ void row_total(float (&v)[4]) {
+  PP_ROW_SUM("quad_perm:[1,0,3,2]");
+  PP_ROW_SUM("quad_perm:[2,3,0,1]");
+  PP_ROW_SUM("row_half_mirror");
+  PP_ROW_SUM("row_mirror");
+  asm volatile("s_nop 1" ::: "memory");   // the results feed ordinary VALU reads / DPP next
 }
 
 // PERSIST: loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
@@ -350,7 +359,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             for (int f = 1; f < 8; ++f) s4 += acc[f >> 2][qn][f & 3][j];
 #pragma unroll
             for (int r = 0; r < 4; ++r) sm[r] = s4[r];
-            row_sum<0xB1>(sm); row_sum<0x4E>(sm); row_sum<0x141>(sm); row_sum<0x140>(sm);
+            row_total(sm);
             f32x4_t mu;
 #pragma unroll
             for (int r = 0; r < 4; ++r) mu[r] = sm[r] * (1.f / 128.f);
@@ -362,7 +371,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) m2[r] = q4[r];
-            row_sum<0xB1>(m2); row_sum<0x4E>(m2); row_sum<0x141>(m2); row_sum<0x140>(m2);
+            row_total(m2);
           } else {
             // ragged last tile: per-lane counts, general merges
             int c = 0;

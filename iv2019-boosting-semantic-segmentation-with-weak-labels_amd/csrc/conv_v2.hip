@@ -120,11 +120,14 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
     a_row[i] = row;
     const long m = m0 + row;
     const bool ok = m < M;
-    const long mm = ok ? m : 0;
-    const int wo = (int)(mm % a.Wo);
-    const long t = mm / a.Wo;
-    const int ho = (int)(t % a.Ho);
-    a_nb[i] = (t / a.Ho) * a.H;
+    // 32-bit decode (M < 2^31: conv_nt_v2_ok); the 64-bit div/rem it replaces was a library
+    // call per row and per tile
+    const unsigned mm = ok ? (unsigned)m : 0u;
+    const unsigned t = mm / (unsigned)a.Wo;
+    const int wo = (int)(mm - t * (unsigned)a.Wo);
+    const unsigned nimg = t / (unsigned)a.Ho;
+    const int ho = (int)(t - nimg * (unsigned)a.Ho);
+    a_nb[i] = (long)nimg * a.H;
     a_h0[i] = ok ? ho * a.sf - a.pad_h : -(1 << 28);  // invalid rows never pass the bounds test
     a_w0[i] = wo * a.sf - a.pad_w;
   }
@@ -447,9 +450,10 @@ bool conv_nt_v2_ok(const ConvArgs& a) {
                 // weights [Co][ldw >= ceil(KH*KW*C/64)*64]
     return a.tap8 == 2 && a.st == 1 && a.C == 16 && a.ldx == 16 && a.Co <= 64 && (a.Co % 8) == 0 &&
            (a.ldy % 8) == 0 && a.ldw >= (a.KH * a.KW * a.C + BK - 1) / BK * BK && (a.ldw % 8) == 0 &&
-           !a.r && !a.r2;
+           !a.r && !a.r2 && (long)a.N * a.Ho * a.Wo < (1L << 31);
   return (a.st == 1 || a.st == 2) && (a.C % BK) == 0 && (a.ldx % 8) == 0 && (a.ldw % 8) == 0 && (a.Co % 8) == 0 &&
-         (a.ldy % 8) == 0 && (!a.r || a.ldr % 8 == 0) && (!a.r2 || a.ldr2 % 8 == 0);
+         (a.ldy % 8) == 0 && (!a.r || a.ldr % 8 == 0) && (!a.r2 || a.ldr2 % 8 == 0) &&
+         (long)a.N * a.Ho * a.Wo < (1L << 31);   // 32-bit pixel decode
 }
 
 // rows per tile of the v2 config launch_conv_nt_v2 picks (= BN-statistics partial rows).
