@@ -45,6 +45,7 @@ enum { SEG_DATASET_CITYSCAPES = 0, SEG_DATASET_VISTAS = 1 };
 enum { SEG_PARAM_WEIGHTS = 0, SEG_PARAM_GAMMA = 1, SEG_PARAM_BETA = 2,
        SEG_PARAM_MOVING_MEAN = 3, SEG_PARAM_MOVING_VAR = 4, SEG_PARAM_BIASES = 5 };
 enum { SEG_UPSAMPLING_BILINEAR = 0, SEG_UPSAMPLING_HYBRID = 1 };
+enum { SEG_NORM_BATCH = 0, SEG_NORM_GROUP = 1 };
 
 typedef struct seg_cfg {
   int depth;            /* 50 | 101 (name_feature_extractor) */
@@ -62,6 +63,10 @@ typedef struct seg_cfg {
                            conv (resnet50_extended_feature_extractor.py:44-49); 0 = off */
   int upsampling;       /* SEG_UPSAMPLING_* (upsampling_method, hierarchical.py:143-184): hybrid
                            adds a 3x3 conv2d_transpose + bias per logits head before the resize */
+  int norm;             /* SEG_NORM_* (norm_layer, hierarchical.py:293-333): group = per-image
+                           tf.contrib.layers.group_norm after every conv, no moving statistics */
+  int groups;           /* group-norm groups of the network's convs (0 = 32); the logits convs
+                           use 1 (the softmax_classifier arg scope) */
 } seg_cfg;
 
 /* lifecycle -------------------------------------------------------------------------- */

@@ -330,13 +330,13 @@ __global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
 #pragma unroll
       for (int e = 0; e < VEC; ++e) dz[e] = z[e] > 0.f ? dz[e] : 0.f;
     }
+    if (DH) {   // the masked gradient before any per-channel factor
+      if constexpr (VEC == 8) Vec8<T>::store(DH + (size_t)m * a.lddyhat + c0, dz);
+      else stf(DH + (size_t)m * a.lddyhat + c0, dz[0]);
+    }
     if (a.dzscale) {
 #pragma unroll
       for (int e = 0; e < VEC; ++e) dz[e] *= a.dzscale[c0 + e];
-    }
-    if (DH) {
-      if constexpr (VEC == 8) Vec8<T>::store(DH + (size_t)m * a.lddyhat + c0, dz);
-      else stf(DH + (size_t)m * a.lddyhat + c0, dz[0]);
     }
     float o[VEC];
 #pragma unroll
@@ -589,16 +589,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwdArgs a) {
   ld8(a.sdy, c0, sdy); ld8(a.sdyx, c0, sdyx);
   T* DY = (T*)a.dy + c0;
   T* DH = (T*)a.dyhat + c0;
+  float ds[8];
+  if constexpr (HS) ld8(a.dzscale, c0, ds);
   const long step = (long)L.rpp * BN_U;
   auto body = [&](long base, int nrows, auto full) {
     float dz[BN_U][8], y[BN_U][8];
     if constexpr (decltype(full)::value) nrows = BN_U;
-    bwd_load<T, TZ, HZ, HS, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
+    bwd_load<T, TZ, HZ, 0, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
 #pragma unroll
     for (int k = 0; k < BN_U; ++k) {
       if (k >= nrows) continue;
       const size_t m = (size_t)(base + k * L.rpp);
+      // dyhat: the masked gradient before the per-channel factor (group norm's gamma)
       if constexpr (HD) BN_STORE8(T, DH + m * a.lddyhat, dz[k]);
+      if constexpr (HS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[k][e] *= ds[e];
+      }
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -684,9 +691,15 @@ hipError_t bwd_apply_t(const BnBwdArgs& a, hipStream_t s) {
   if (bwd_v8<T, TZ>(a)) {
     const dim3 g = grid8(a.M, a.C);
     const int key = (a.z ? 4 : 0) | (a.dzscale ? 2 : 0) | (a.dyhat ? 1 : 0);
-    if (a.mask) {   // ReLU bits (never combined with dzscale: that is the logits BN, no ReLU)
-      if (a.dyhat) hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 0, 1>), g, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 0, 0>), g, dim3(256), 0, s, a);
+    if (a.mask) {   // ReLU bits; dzscale with them only under group norm (gamma)
+      if (a.dzscale) {
+        if (a.dyhat) hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 1, 1>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 1, 0>), g, dim3(256), 0, s, a);
+      } else if (a.dyhat) {
+        hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 0, 1>), g, dim3(256), 0, s, a);
+      } else {
+        hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 0, 0>), g, dim3(256), 0, s, a);
+      }
       return hipGetLastError();
     }
     switch (key) {

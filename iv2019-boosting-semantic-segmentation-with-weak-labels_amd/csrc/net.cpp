@@ -17,6 +17,7 @@
 #include "input.h"
 #include "conv.h"
 #include "deconv.h"
+#include "gn.h"
 #include "loss.h"
 #include "labels.h"
 #include "optim.h"
@@ -58,8 +59,14 @@ struct ConvL {
   Act y, dy;                      // conv output and its gradient
   BnState st{};
   float* stats_part = nullptr;    // [mtiles][co][2]
-  float* bwd_part = nullptr;      // [rb][co][2]
+  float* bwd_part = nullptr;      // [rb][co][2] (group norm: [N][rb][co][2], rb per image)
   int rb = 1;
+  // group norm: groups, per-image states (host copies of the device array st_dev) and the
+  // forward chunk partials
+  int groups = 0;
+  std::vector<BnState> st_img;
+  BnState* st_dev = nullptr;
+  float* gn_part = nullptr;
 };
 
 enum ShortcutKind { SC_IDENTITY = 0, SC_SUBSAMPLE = 1, SC_CONV = 2 };
@@ -144,6 +151,8 @@ struct seg_ctx {
   int logit_conv[3] = {-1, -1, -1};
   Act logits;                     // fp32 [N][Hl][Wl][ldl]
   float* grad_un = nullptr;       // fp32 same shape (gradient w.r.t. head_in)
+  bool gn = false;                // norm_layer = group (gn.h)
+  float* gn_gscaled = nullptr;    // group norm: the logits gradient times the loss factors
   // 'hybrid' upsampling: per-head 3x3 conv2d_transpose + bias on the logits (deconv.h)
   bool hybrid = false;
   long dc_w_off[3] = {0, 0, 0}, dc_b_off[3] = {0, 0, 0}, dc_b_lo = 0;
@@ -379,8 +388,24 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
   L.st.sdy = v + 4 * L.co; L.st.sdyx = v + 5 * L.co;
   long M = (long)N * L.Ho * L.Wo;
   if (int r = dalloc(c, &L.stats_part, (size_t)conv_nt_mtiles(M) * L.co * 2)) return r;
-  L.rb = bn_bwd_rowblocks(M, L.co);
-  if (int r = dalloc(c, &L.bwd_part, (size_t)L.rb * L.co * 2)) return r;
+  if (c->gn) {
+    const long hw = (long)L.Ho * L.Wo;
+    L.rb = bn_bwd_rowblocks(hw, L.co);
+    if (int r = dalloc(c, &L.bwd_part, (size_t)N * L.rb * L.co * 2)) return r;
+    if (int r = dalloc(c, &L.gn_part, (size_t)N * gn_chunks(hw) * L.co * 2)) return r;
+    float* sv;
+    if (int r = dalloc(c, &sv, (size_t)N * 6 * L.co)) return r;
+    L.st_img.resize(N);
+    for (int n = 0; n < N; ++n) {
+      float* b = sv + (size_t)n * 6 * L.co;
+      L.st_img[n] = BnState{b, b + L.co, b + 2 * L.co, b + 3 * L.co, b + 4 * L.co, b + 5 * L.co};
+    }
+    if (int r = dalloc(c, &L.st_dev, (size_t)N)) return r;
+    HIPCALL(c, hipMemcpy(L.st_dev, L.st_img.data(), N * sizeof(BnState), hipMemcpyHostToDevice));
+  } else {
+    L.rb = bn_bwd_rowblocks(M, L.co);
+    if (int r = dalloc(c, &L.bwd_part, (size_t)L.rb * L.co * 2)) return r;
+  }
   size_t need = (size_t)((conv_nt_mtiles(M) + 63) / 64) * L.co * 3;
   c->stat_scratch_floats = std::max(c->stat_scratch_floats, need);
   return 0;
@@ -461,6 +486,14 @@ int conv_forward(Step& S, int li, const Act& x) {
   if (int r = prof_begin(c, S.s, 0, li, 2.0 * M * L.co * L.k * L.k * L.ci * 1e-9, &slot, gbx)) return r;
   HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
+  if (c->gn) {   // group norm: per-image statistics in every mode (no moving statistics)
+    GnPartArgs g{};
+    g.y = L.y.p; g.ldy = L.y.ld; g.N = x.N; g.hw = (long)L.Ho * L.Wo; g.C = L.co; g.part = L.gn_part;
+    HIPCALL(c, launch_gn_partial(S.dt, 0, g, S.s));
+    HIPCALL(c, launch_gn_stats_final(L.gn_part, x.N, g.hw, L.co, L.groups, c->params + L.g_off,
+                                     L.st_dev, S.s));
+    return 0;
+  }
   if (c->bn_infer) return 0;   // is_training=False: the statistics were set for every layer
                                // by one launch at the start of the forward
   const bool sync = c->sync_fn != nullptr;
@@ -475,13 +508,42 @@ int conv_forward(Step& S, int li, const Act& x) {
 }
 
 // out = act(bn(y) [+ residual])
+int bn_apply_one(Step& S, int li, const Act& out, int out_f32, const Act* res, int rs, int li2,
+                 int relu, int img);
+
 int bn_apply(Step& S, int li, const Act& out, int out_f32, const Act* res = nullptr, int rs = 1,
              int li2 = -1, int relu = -1) {
+  if (!S.c->gn) return bn_apply_one(S, li, out, out_f32, res, rs, li2, relu, -1);
+  // group norm: the per-image affine is per channel; one launch per image on row offsets
+  for (int n = 0; n < out.N; ++n)
+    if (int r = bn_apply_one(S, li, out, out_f32, res, rs, li2, relu, n)) return r;
+  return 0;
+}
+
+// one image's rows of an activation (img < 0: all of it)
+Act image_rows(const Act& a, int img, size_t esz) {
+  if (img < 0) return a;
+  Act v = a;
+  const size_t hw = (size_t)a.H * a.W;
+  v.p = (char*)a.p + (size_t)img * hw * a.ld * esz;
+  if (a.mask) v.mask = a.mask + (size_t)img * hw * (a.C / 8);
+  v.N = 1;
+  return v;
+}
+
+int bn_apply_one(Step& S, int li, const Act& out0, int out_f32, const Act* res0, int rs, int li2,
+                 int relu, int img) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
+  const Act out = image_rows(out0, img, out_f32 ? 4 : c->esz);
+  Act res_img;
+  const Act* res = res0;
+  if (res0 && img >= 0) { res_img = image_rows(*res0, img, c->esz); res = &res_img; }
+  const Act Y = image_rows(L.y, img, c->esz);
+  const BnState& st = img >= 0 ? L.st_img[img] : L.st;
   BnApplyArgs a{};
-  a.y = L.y.p; a.ldy = L.y.ld; a.M = L.y.M(); a.C = L.co;
-  a.mean = L.st.mean; a.scale = L.st.scale; a.beta = c->params + L.b_off;
+  a.y = Y.p; a.ldy = Y.ld; a.M = Y.M(); a.C = L.co;
+  a.mean = st.mean; a.scale = st.scale; a.beta = c->params + L.b_off;
   a.relu = relu < 0 ? (L.relu ? 1 : 0) : relu;
   if (res) {
     a.res = res->p; a.ldres = res->ld; a.rs = rs; a.Ho = L.Ho; a.Wo = L.Wo; a.Hr = res->H;
@@ -489,7 +551,9 @@ int bn_apply(Step& S, int li, const Act& out, int out_f32, const Act* res = null
   }
   if (li2 >= 0) {
     ConvL& L2 = c->convs[li2];
-    a.y2 = L2.y.p; a.ldy2 = L2.y.ld; a.mean2 = L2.st.mean; a.scale2 = L2.st.scale;
+    const Act Y2 = image_rows(L2.y, img, c->esz);
+    const BnState& st2 = img >= 0 ? L2.st_img[img] : L2.st;
+    a.y2 = Y2.p; a.ldy2 = Y2.ld; a.mean2 = st2.mean; a.scale2 = st2.scale;
     a.beta2 = c->params + L2.b_off;
   }
   a.out = out.p; a.ldo = out.ld;
@@ -503,10 +567,14 @@ int bn_apply(Step& S, int li, const Act& out, int out_f32, const Act* res = null
   return prof_end(c, S.s, slot);
 }
 
+int gn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const Act* dyhat_out,
+                const float* dzscale);
+
 // BN backward for layer li: dz (gradient wrt BN output), z (mask source or null)
 int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const Act* dyhat_out,
                 const float* dzscale = nullptr) {
   seg_ctx* c = S.c;
+  if (c->gn) return gn_backward(S, li, dz, dz_f32, z, dyhat_out, dzscale);
   ConvL& L = c->convs[li];
   BnBwdArgs a{};
   a.dz = dz.p; a.lddz = dz.ld;
@@ -541,6 +609,58 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   if (int r = prof_begin(c, S.s, 5, li, gb_apply, &slot)) return r;
   HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
   return prof_end(c, S.s, slot);
+}
+
+// group norm backward (gn.h): per image the batch-norm reduce (S1, S2 per channel) into
+// its slice of the partials, one finalize for the layer (dgamma / dbeta, per-image group
+// means), per image the batch-norm apply with scale = invstd and the gradient times gamma
+int gn_backward(Step& S, int li, const Act& dz0, int dz_f32, const Act* z0, const Act* dyhat0,
+                const float* dzscale) {
+  seg_ctx* c = S.c;
+  ConvL& L = c->convs[li];
+  const size_t zsz = dz_f32 ? 4 : c->esz;
+  Act dzl = dz0;
+  if (dzscale) {   // the logits: the loss normalisation first (gamma mixes into it below)
+    HIPCALL(c, launch_gn_chscale((const float*)dz0.p, c->gn_gscaled, dz0.M(), dz0.ld, L.co, dzscale, S.s));
+    dzl.p = c->gn_gscaled;
+  }
+  const float* gamma = c->params + L.g_off;
+  const bool tb = c->cfg.train_bn != 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1)
+      HIPCALL(c, launch_gn_bwd_final(L.bwd_part, dz0.N, L.rb, (long)L.Ho * L.Wo, L.co, L.groups, gamma,
+                                     L.st_dev, tb ? c->grads + L.g_off : nullptr,
+                                     tb ? c->grads + L.b_off : nullptr, S.s));
+    for (int n = 0; n < dz0.N; ++n) {
+      const Act dz = image_rows(dzl, n, zsz);
+      const Act Y = image_rows(L.y, n, c->esz);
+      const Act DY = image_rows(L.dy, n, c->esz);
+      const BnState& st = L.st_img[n];
+      BnBwdArgs a{};
+      a.dz = dz.p; a.lddz = dz.ld;
+      if (z0) {
+        const Act z = image_rows(*z0, n, zsz);
+        a.z = z.p; a.ldz = z.ld;
+        if (z.mask && !dz_f32 && z.C == L.co) { a.mask = z.mask; a.z = nullptr; }
+      }
+      a.y = Y.p; a.ldy = Y.ld; a.M = Y.M(); a.C = L.co;
+      a.mean = st.mean; a.invstd = st.invstd; a.sdy = st.sdy; a.sdyx = st.sdyx;
+      a.dy = DY.p; a.lddy = DY.ld;
+      a.part = L.bwd_part + (size_t)n * L.rb * L.co * 2; a.rb = L.rb;
+      if (pass == 0) {
+        HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
+      } else {
+        if (dyhat0) {
+          const Act dh = image_rows(*dyhat0, n, c->esz);
+          a.dyhat = dh.p; a.lddyhat = dh.ld;
+        }
+        a.scale = st.invstd;   // dx = invstd (gamma dyhat - sdy - xhat sdyx)
+        a.dzscale = gamma;
+        HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
+      }
+    }
+  }
+  return 0;
 }
 
 // dx = dgrad(dy) [+ r1] [+ r2]
@@ -779,6 +899,20 @@ int build(seg_ctx* c) {
   if (g.upsampling != SEG_UPSAMPLING_BILINEAR && g.upsampling != SEG_UPSAMPLING_HYBRID)
     return set_err(&c->err, -EINVAL, "upsampling must be bilinear or hybrid");
   c->hybrid = g.upsampling == SEG_UPSAMPLING_HYBRID;
+  if (g.norm != SEG_NORM_BATCH && g.norm != SEG_NORM_GROUP)
+    return set_err(&c->err, -EINVAL, "norm must be batch or group");
+  c->gn = g.norm == SEG_NORM_GROUP;
+  if (c->gn) {   // module_arg_scope groups (32), the softmax_classifier scope's groups=1
+    const int G = g.groups > 0 ? g.groups : 32;
+    for (auto& L : c->convs) {
+      const bool logit = &L == &c->convs[c->logit_conv[0]] || &L == &c->convs[c->logit_conv[1]] ||
+                         &L == &c->convs[c->logit_conv[2]];
+      L.groups = logit ? 1 : G;
+      if (L.co % L.groups || L.co / L.groups > 256)
+        return set_err(&c->err, -EINVAL, "group norm: %s has %d channels for %d groups", L.name.c_str(),
+                       L.co, L.groups);
+    }
+  }
 
   // ---- flat parameter layout ----
   // [conv weights | hybrid deconv weights] (weight decay) [BN gamma/beta | deconv biases]
@@ -825,6 +959,11 @@ int build(seg_ctx* c) {
   }
   for (auto& L : c->convs) {
     c->pinfo.push_back({L.name + "/weights", L.w_off, (long)L.co * L.k * L.k * L.ci, SEG_PARAM_WEIGHTS, {L.co, L.k, L.k, L.ci}});
+    if (c->gn) {   // tf.contrib.layers.group_norm variables: no moving statistics
+      c->pinfo.push_back({L.name + "/GroupNorm/beta", L.b_off, L.co, SEG_PARAM_BETA, {L.co, 1, 1, 1}});
+      c->pinfo.push_back({L.name + "/GroupNorm/gamma", L.g_off, L.co, SEG_PARAM_GAMMA, {L.co, 1, 1, 1}});
+      continue;
+    }
     c->pinfo.push_back({L.name + "/BatchNorm/beta", L.b_off, L.co, SEG_PARAM_BETA, {L.co, 1, 1, 1}});
     c->pinfo.push_back({L.name + "/BatchNorm/gamma", L.g_off, L.co, SEG_PARAM_GAMMA, {L.co, 1, 1, 1}});
     c->pinfo.push_back({L.name + "/BatchNorm/moving_mean", L.mv_off, L.co, SEG_PARAM_MOVING_MEAN, {L.co, 1, 1, 1}});
@@ -944,6 +1083,8 @@ int build(seg_ctx* c) {
   if (int r = alloc_act(c, c->logits, N, Hf, Wf, c->nc[0] + c->nc[1] + c->nc[2], c->ldl, 4)) return r;
   if (int r = dalloc(c, &c->grad_un, (size_t)N * Hf * Wf * c->ldl)) return r;
   c->head_in = (const float*)c->logits.p;
+  if (c->gn)
+    if (int r = dalloc(c, &c->gn_gscaled, (size_t)N * Hf * Wf * c->ldl)) return r;
   if (c->hybrid) {
     if (int r = dalloc(c, &c->up_in, (size_t)N * Hf * Wf * c->ldl)) return r;
     if (int r = dalloc(c, &c->dc_dx, (size_t)N * Hf * Wf * c->ldl)) return r;
@@ -1395,6 +1536,7 @@ int seg_loss(seg_ctx* c, const int32_t* px, const float* bbox, const float* tag,
 
 int seg_set_bn_inference(seg_ctx* c, int on) {
   if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (c->gn) return 0;   // group norm normalises every image by its own statistics in all modes
   if (on) {   // (re)build the per-layer job table from the bound buffers (outside any step)
     NEED_BOUND(c);
     std::vector<BnInferJob> jobs;
@@ -1490,8 +1632,9 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
     HIPCALL(c, launch_sgdm(b, s));
   }
   const long half = c->n_moving / 2;
-  HIPCALL(c, launch_moving_update(c->moving, c->moving + half, c->grads + c->n_train,
-                                  c->grads + c->n_train + half, (int)half, c->cfg.bn_decay, s));
+  if (!c->gn)   // group norm keeps no moving statistics
+    HIPCALL(c, launch_moving_update(c->moving, c->moving + half, c->grads + c->n_train,
+                                    c->grads + c->n_train + half, (int)half, c->cfg.bn_decay, s));
   if (c->n_flip) HIPCALL(c, launch_weight_flip_batched(c->dt, c->flip_jobs, c->n_flip, c->flip_total, s));
   return refresh_stem_pad(c, s);
 }
@@ -1534,6 +1677,8 @@ int seg_set_loss_scale(seg_ctx* c, float scale) {
 
 int seg_set_bn_sync(seg_ctx* c, seg_allreduce_fn fn, void* user, int world) {
   if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  if (c->gn && fn && world > 1)   // module_arg_scope :329-331
+    return set_err(&c->err, -EINVAL, "cross_replica_norm is supported only for batch normalization");
   if (world < 1) return set_err(&c->err, -EINVAL, "world must be >= 1");
   if (!fn || world == 1) {
     c->sync_fn = nullptr;

@@ -38,7 +38,7 @@ def init_params(param_info, seed=0):
             conv_index += 1
             fan_in = shape[1] * shape[2] * shape[3]
             out[p.name] = _truncated_normal(rng, shape, math.sqrt(1.3 * 2.0 / fan_in)).astype(np.float32)
-        elif p.kind == 'gamma' or p.kind == 'moving_variance':
+        elif p.kind == 'gamma' or p.kind == 'moving_variance':   # BatchNorm or GroupNorm gamma
             out[p.name] = np.ones(p.numel, np.float32)
         else:
             out[p.name] = np.zeros(p.numel, np.float32)

@@ -41,8 +41,11 @@ def _validate_params(params):
         # 'no' leaves the logits at H/8 x W/8, which the reference's own losses cannot
         # compare with full-resolution labels
         raise NotImplementedError("upsampling_method must be 'bilinear' (default) or 'hybrid'")
-    if getattr(params, 'norm_layer', 'batch') != 'batch':
-        raise NotImplementedError("only norm_layer='batch' is implemented")
+    if getattr(params, 'norm_layer', 'batch') not in ('batch', 'group'):
+        raise ValueError('norm_type not valid.')   # module_arg_scope :291-292
+    if getattr(params, 'norm_layer', 'batch') == 'group' and getattr(params, 'cross_replica_norm', False):
+        # module_arg_scope :329-331
+        raise ValueError('cross_replica_norm is supported only for batch normalization for now.')
     if getattr(params, 'stride_feature_extractor', 8) != 8:
         raise NotImplementedError('stride_feature_extractor must be 8')
 
@@ -72,7 +75,7 @@ def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
            params.per_pixel_dataset_name, bool(getattr(params, 'cross_replica_norm', False)),
            getattr(params, 'ema_decay', 0) > 0,
            getattr(params, 'fov_expansion_kernel_size', 0), getattr(params, 'fov_expansion_kernel_rate', 0),
-           getattr(params, 'upsampling_method', 'bilinear'))
+           getattr(params, 'upsampling_method', 'bilinear'), getattr(params, 'norm_layer', 'batch'))
     ctx = _CONTEXTS.get(key)
     if ctx is None:
         ctx = SegContext(depth=depth, pyramid=pyramid, height=params.height_feature_extractor,
@@ -88,7 +91,10 @@ def get_context(config, params, device=None, mode=ModeKeys.TRAIN):
                          fov_k=getattr(params, 'fov_expansion_kernel_size', 0),
                          fov_rate=getattr(params, 'fov_expansion_kernel_rate', 0),
                          # 'hybrid': conv2d_transpose + bias per head (hierarchical.py:168-180)
-                         upsampling=getattr(params, 'upsampling_method', 'bilinear'))
+                         upsampling=getattr(params, 'upsampling_method', 'bilinear'),
+                         # norm_layer='group': group_norm(groups=32) after every conv, groups=1
+                         # on the logits (hierarchical.py:44-48,78,293-333)
+                         norm=getattr(params, 'norm_layer', 'batch'))
         ctx.load_params(init_params(ctx.param_info, seed=getattr(params, 'init_seed', 0)))
         if getattr(params, 'cross_replica_norm', False):
             # hierarchical.py:327-328: BN statistics over all replicas (torch.distributed)

@@ -41,6 +41,7 @@ DATASET = {"cityscapes": 0, "vistas": 1}
 PARAM_KIND = {0: "weights", 1: "gamma", 2: "beta", 3: "moving_mean", 4: "moving_variance",
               5: "biases"}
 UPSAMPLING = {"bilinear": 0, "hybrid": 1}
+NORM = {"batch": 0, "group": 1}
 
 
 class SegCfg(ctypes.Structure):
@@ -51,7 +52,7 @@ class SegCfg(ctypes.Structure):
         ("output_stride", ctypes.c_int), ("feature_dims", ctypes.c_int),
         ("bn_decay", ctypes.c_float), ("train_bn", ctypes.c_int),
         ("weight_decay", ctypes.c_float), ("fov_k", ctypes.c_int), ("fov_rate", ctypes.c_int),
-        ("upsampling", ctypes.c_int),
+        ("upsampling", ctypes.c_int), ("norm", ctypes.c_int), ("groups", ctypes.c_int),
     ]
 
 
@@ -163,13 +164,14 @@ class SegContext:
     def __init__(self, *, depth=50, pyramid="psp", height=512, width=1024, nb_pp=2, nb_pb=0,
                  nb_pi=0, dtype="bf16", dataset="cityscapes", output_stride=8,
                  feature_dims=256, bn_decay=0.9, train_bn=True, weight_decay=0.00017,
-                 ema=False, device=None, fov_k=0, fov_rate=0, upsampling="bilinear"):
+                 ema=False, device=None, fov_k=0, fov_rate=0, upsampling="bilinear",
+                 norm="batch", groups=0):
         import torch
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         self.cfg = SegCfg(depth, PYRAMID[pyramid], height, width, nb_pp, nb_pb, nb_pi,
                           DTYPE[dtype], DATASET[dataset], output_stride, feature_dims,
                           bn_decay, int(bool(train_bn)), weight_decay, fov_k, fov_rate,
-                          UPSAMPLING[upsampling])
+                          UPSAMPLING[upsampling], NORM[norm], groups)
         self.dtype = dtype
         h = ctypes.c_void_p()
         check(LIB.seg_create(self.device.index, ctypes.byref(self.cfg), ctypes.byref(h)))

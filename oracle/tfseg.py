@@ -39,6 +39,7 @@ import torch.nn.functional as F
 # ----------------------------------------------------------------------------------------
 
 BN_EPS = 1.001e-5  # tf.nn.fused_batch_norm clamps epsilon=1e-5 (hierarchical.py:335) up to this
+GN_EPS = 1e-5      # group_norm takes norm_epsilon as given (hierarchical.py:313-317)
 
 
 @dataclass
@@ -58,6 +59,8 @@ class SegConfig:
     fov_k: int = 0                   # fov_expansion_kernel_size (hierarchical.py:247-250)
     fov_rate: int = 0                # fov_expansion_kernel_rate
     upsampling: str = "bilinear"     # upsampling_method (hierarchical.py:143-184): bilinear | hybrid
+    norm: str = "batch"              # norm_layer (hierarchical.py:293-333): batch | group
+    groups: int = 32                 # module_arg_scope groups (group norm; logits use 1)
 
     @property
     def nb(self) -> int:
@@ -193,6 +196,10 @@ def init_params(cfg: SegConfig, seed: int = 0) -> Dict[str, np.ndarray]:
         fan_in = s.k * s.k * s.ci
         p[f"{s.name}/weights"] = truncated_normal(rng, (s.co, s.k, s.k, s.ci),
                                                  math.sqrt(1.3 * 2.0 / fan_in))
+        if cfg.norm == "group":   # tf.contrib.layers.group_norm: gamma / beta only
+            p[f"{s.name}/GroupNorm/gamma"] = np.ones(s.co)
+            p[f"{s.name}/GroupNorm/beta"] = np.zeros(s.co)
+            continue
         p[f"{s.name}/BatchNorm/gamma"] = np.ones(s.co)
         p[f"{s.name}/BatchNorm/beta"] = np.zeros(s.co)
         p[f"{s.name}/BatchNorm/moving_mean"] = np.zeros(s.co)
@@ -442,6 +449,22 @@ class OracleNet:
     def conv_bn(self, x, name: str, relu: Optional[bool] = None, record: Dict = None):
         s = self.spec_by_name[name]
         y = conv_tf(x, self.p[f"{name}/weights"], s)
+        if self.cfg.norm == "group":
+            # tf.contrib.layers.group_norm (module_arg_scope :313-333): per image, moments over
+            # H x W x C/G (tf.nn.moments: biased), epsilon 1e-5; the softmax_classifier scope
+            # passes groups=1 (hierarchical.py:78)
+            G = 1 if name.startswith("softmax_classifier/") else self.cfg.groups
+            n, c, h, w = y.shape
+            yg = y.reshape(n, G, c // G, h, w)
+            mean = yg.mean(dim=(2, 3, 4), keepdim=True)
+            var = ((yg - mean) ** 2).mean(dim=(2, 3, 4), keepdim=True)
+            xh = ((yg - mean) * torch.rsqrt(var + GN_EPS)).reshape(n, c, h, w)
+            out = xh * self.p[f"{name}/GroupNorm/gamma"][None, :, None, None] + \
+                self.p[f"{name}/GroupNorm/beta"][None, :, None, None]
+            if record is not None:
+                record[name] = y
+            act = s.relu if relu is None else relu
+            return torch.relu(out) if act else out
         if self.bn_inference:   # is_training=False (hierarchical.py:306-307): moving statistics
             mm = self.p[f"{name}/BatchNorm/moving_mean"]
             mv = self.p[f"{name}/BatchNorm/moving_variance"]

@@ -38,7 +38,8 @@ def _native_step(cuda, cfg, params, data, dtype, lr=0.01, steps=1):
     ctx = SegContext(depth=cfg.depth, pyramid=cfg.pyramid, height=cfg.height, width=cfg.width,
                      nb_pp=cfg.nb_pp, nb_pb=cfg.nb_pb, nb_pi=cfg.nb_pi, dtype=dtype,
                      weight_decay=cfg.weight_decay, bn_decay=cfg.bn_decay,
-                     fov_k=cfg.fov_k, fov_rate=cfg.fov_rate, upsampling=cfg.upsampling)
+                     fov_k=cfg.fov_k, fov_rate=cfg.fov_rate, upsampling=cfg.upsampling,
+                     norm=cfg.norm, groups=cfg.groups)
     ctx.load_params(params)
     img = torch.as_tensor(data["images"]).to(cuda)
     px = torch.as_tensor(data["px"]).to(cuda) if cfg.nb_pp else None
@@ -80,10 +81,13 @@ CONFIGS = [
     SegConfig(height=48, width=64, nb_pp=2, pyramid="psp", fov_k=3, fov_rate=2),
     # upsampling_method='hybrid' (hierarchical.py:168-180): 3x3 conv2d_transpose + bias per head
     SegConfig(height=48, width=64, nb_pp=1, nb_pb=1, pyramid="none", upsampling="hybrid"),
+    # norm_layer='group' (hierarchical.py:293-333): group_norm(32) everywhere, groups=1 on the
+    # logits, PSP branches normalised over their pooled grids
+    SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="psp", norm="group"),
 ]
 
 
-@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"r{c.depth}-{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}" + (f"-fov{c.fov_k}r{c.fov_rate}" if c.fov_k else "") + ("-hybrid" if c.upsampling == "hybrid" else ""))
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"r{c.depth}-{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}" + (f"-fov{c.fov_k}r{c.fov_rate}" if c.fov_k else "") + ("-hybrid" if c.upsampling == "hybrid" else "") + ("-gn" if c.norm == "group" else ""))
 def test_train_step_fp32(cuda, cfg):
     from input_pipelines.synthetic import batch
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=3).items()}
@@ -370,4 +374,57 @@ def test_fp16_loss_scaling_unscales_and_skips_overflow(cuda):
     g3, p3, f3 = step(1e38, 0.01)
     assert f3 == 1
     assert torch.equal(p3, p0)
+    ctx.close()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_group_norm_layerwise(cuda, dtype):
+    """norm_layer='group' in 16-bit storage, layer by layer: every conv on its native input (as
+    test_bf16_layerwise), and every bottleneck's conv2 / conv3 input against relu(group_norm(y))
+    of the previous conv's native output (per image, 32 groups, biased variance, eps 1e-5,
+    tf.contrib.layers.group_norm)."""
+    from input_pipelines.synthetic import batch
+    from oracle.tfseg import GN_EPS, build_specs, conv_tf
+    from seg_hip import SegContext
+    cfg = SegConfig(height=64, width=128, nb_pp=2, nb_pb=1, pyramid="aspp", norm="group")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=5).items()}
+    rng = np.random.default_rng(2)
+    for k in params:   # non-trivial affine parameters
+        if k.endswith("/gamma"):
+            params[k] = (1.0 + 0.2 * rng.standard_normal(params[k].shape)).astype(np.float32)
+        elif k.endswith("/beta"):
+            params[k] = (0.2 * rng.standard_normal(params[k].shape)).astype(np.float32)
+    data = batch(12, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
+    ctx = SegContext(pyramid="aspp", height=64, width=128, nb_pp=2, nb_pb=1, dtype=dtype, norm="group")
+    ctx.load_params(params)
+    dev = lambda a: None if a is None else torch.as_tensor(a).to(cuda)
+    ctx.forward(torch.as_tensor(data["images"]).to(cuda))
+    ctx.loss(dev(data["px"]), dev(data["bbox"]), None)
+    lv = ctx.outputs()[0].cpu().numpy()
+    assert np.all(np.isfinite(lv)) and 0.5 < lv[1] < 10.0
+    specs = build_specs(cfg)
+    idx = {s.name: i for i, s in enumerate(specs)}
+    tol = 1e-2 if dtype == "bf16" else 2e-3
+    checked = 0
+    for i, s in enumerate(specs):
+        x = torch.as_tensor(ctx.debug_tensor(f"conv{i}_x"), dtype=torch.float64).permute(0, 3, 1, 2)
+        w = torch.as_tensor(params[s.name + "/weights"]).to(HALF[dtype]).double()
+        ref = conv_tf(x, w, s).permute(0, 2, 3, 1).numpy()
+        y = ctx.debug_tensor(f"conv{i}_y")
+        assert _rel(y, ref) < tol, (s.name, _rel(y, ref))
+        for a_, b_ in (("conv1", "conv2"), ("conv2", "conv3")):
+            nxt = s.name[:-len(a_)] + b_
+            if s.name.endswith("/" + a_) and nxt in idx:   # (not the stem, .../resnet_v1_50/conv1)
+                yt = torch.as_tensor(y, dtype=torch.float64)                 # [n, h, w, c]
+                n_, h_, w_, c_ = yt.shape
+                yg = yt.reshape(n_, h_ * w_, 32, c_ // 32)
+                mu = yg.mean(dim=(1, 3), keepdim=True)
+                var = ((yg - mu) ** 2).mean(dim=(1, 3), keepdim=True)
+                z = ((yg - mu) / torch.sqrt(var + GN_EPS)).reshape(n_, h_, w_, c_)
+                z = torch.relu(z * torch.as_tensor(params[s.name + "/GroupNorm/gamma"], dtype=torch.float64)
+                               + torch.as_tensor(params[s.name + "/GroupNorm/beta"], dtype=torch.float64))
+                xn = ctx.debug_tensor(f"conv{idx[nxt]}_x")
+                assert _rel(xn, z.numpy()) < tol, (s.name, _rel(xn, z.numpy()))
+                checked += 1
+    assert checked == 2 * (16 + 3)
     ctx.close()

@@ -309,3 +309,29 @@ def test_hybrid_deconv_matches_tf_conv2d_transpose_definition():
     net = OracleNet(cfg, p)
     low = net.forward(torch.zeros(1, 64, 128, 3, dtype=torch.float64))
     assert low["l1_logits"].shape == (1, 14, 8, 16)
+
+
+def test_group_norm_restatement_matches_torch_group_norm():
+    """The oracle's group norm (tf.contrib.layers.group_norm semantics: per image, moments
+    over H x W x C/G, biased variance, epsilon 1e-5) equals torch.nn.functional.group_norm;
+    the logits use one group (softmax_classifier arg scope, hierarchical.py:78); no moving
+    statistics are created (names under GroupNorm/)."""
+    cfg = SegConfig(height=64, width=128, pyramid="none", norm="group")
+    p = tfseg.init_params(cfg, seed=2)
+    assert not any("moving" in k or "BatchNorm" in k for k in p)
+    rng = np.random.default_rng(0)
+    for k in p:
+        if k.endswith("/gamma") or k.endswith("/beta"):
+            p[k] = rng.standard_normal(p[k].shape)
+    net = OracleNet(cfg, p)
+    x = torch.tensor(rng.standard_normal((2, 256, 8, 16)))
+    name = "adaptation_module/l1_features/conv1"
+    got = net.conv_bn(x, name, relu=False)
+    y = tfseg.conv_tf(x, net.p[name + "/weights"], net.spec_by_name[name])
+    ref = F.group_norm(y, 32, net.p[name + "/GroupNorm/gamma"], net.p[name + "/GroupNorm/beta"], eps=1e-5)
+    assert torch.allclose(got, ref, rtol=1e-10, atol=1e-10)
+    lg = "softmax_classifier/l1_logits"
+    got = net.conv_bn(x, lg, relu=False)
+    y = tfseg.conv_tf(x, net.p[lg + "/weights"], net.spec_by_name[lg])
+    ref = F.group_norm(y, 1, net.p[lg + "/GroupNorm/gamma"], net.p[lg + "/GroupNorm/beta"], eps=1e-5)
+    assert torch.allclose(got, ref, rtol=1e-10, atol=1e-10)
