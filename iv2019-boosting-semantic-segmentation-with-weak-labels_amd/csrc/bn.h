@@ -62,8 +62,10 @@ hipError_t launch_bn_infer_finalize(const float* mov_mean, const float* mov_var,
 hipError_t launch_bn_apply(int dtype, int out_f32, const BnApplyArgs& a, hipStream_t s);
 int bn_bwd_rowblocks(long M, int C);
 hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipStream_t s);
+// frozen: is_training=False statistics (moving averages): the batch means do not depend on
+// the input, so sdy = sdyx = 0 and dy = gamma * invstd * dyhat (FusedBatchNormGrad, inference)
 hipError_t launch_bn_bwd_finalize(const float* part, int rb, long M, int C, BnState st,
-                                  float* dgamma, float* dbeta, hipStream_t s);
+                                  float* dgamma, float* dbeta, hipStream_t s, int frozen = 0);
 hipError_t launch_bn_bwd_apply(int dtype, int dz_f32, const BnBwdArgs& a, hipStream_t s);
 hipError_t launch_moving_update(float* mov_mean, float* mov_var, const float* bmean,
                                 const float* bvar, int n, float decay, hipStream_t s);

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(FIN_CH * FIN_LANES) void bn_stats_final_kernel(
 // layout and fixed reduction order
 __global__ __launch_bounds__(FIN_CH * FIN_LANES) void bn_bwd_final_kernel(
     const float* __restrict__ part, int rb, long M, int C, BnState st, float* dgamma,
-    float* dbeta) {
+    float* dbeta, int frozen) {
   __shared__ float sh[2][FIN_LANES / 8][FIN_CH];
   const int cl = threadIdx.x % FIN_CH, tl = threadIdx.x / FIN_CH;
   const int c = blockIdx.x * FIN_CH + cl;
@@ -127,8 +127,8 @@ __global__ __launch_bounds__(FIN_CH * FIN_LANES) void bn_bwd_final_kernel(
       s1 += sh[0][k][cl];
       s2 += sh[1][k][cl];
     }
-    st.sdy[c] = s1 / (float)M;
-    st.sdyx[c] = s2 / (float)M;
+    st.sdy[c] = frozen ? 0.f : s1 / (float)M;
+    st.sdyx[c] = frozen ? 0.f : s2 / (float)M;
     if (dgamma) dgamma[c] = s2;
     if (dbeta) dbeta[c] = s1;
   }
@@ -783,9 +783,9 @@ hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipSt
 }
 
 hipError_t launch_bn_bwd_finalize(const float* part, int rb, long M, int C, BnState st,
-                                  float* dgamma, float* dbeta, hipStream_t s) {
+                                  float* dgamma, float* dbeta, hipStream_t s, int frozen) {
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ceil_div(C, FIN_CH)), dim3(FIN_CH * FIN_LANES), 0, s,
-                     part, rb, M, C, st, dgamma, dbeta);
+                     part, rb, M, C, st, dgamma, dbeta, frozen);
   return hipGetLastError();
 }
 

@@ -595,10 +595,12 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
   const bool tb = c->cfg.train_bn != 0;
+  // a backward after a moving-statistics forward (TRAIN without
+  // batch_norm_accumulate_statistics) differentiates through constant statistics
   HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
                                     tb ? c->grads + L.g_off : nullptr,
-                                    tb ? c->grads + L.b_off : nullptr, S.s));
-  if (c->sync_fn) {
+                                    tb ? c->grads + L.b_off : nullptr, S.s, c->bn_infer));
+  if (c->sync_fn && !c->bn_infer) {
     // [mean(dyhat) | mean(dyhat * xhat)] (contiguous in the layer's state) averaged over the
     // replicas: dx is the gradient through the global statistics; dgamma / dbeta stay this
     // replica's sums (the gradient all-reduce averages them)
@@ -1632,7 +1634,8 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
     HIPCALL(c, launch_sgdm(b, s));
   }
   const long half = c->n_moving / 2;
-  if (!c->gn)   // group norm keeps no moving statistics
+  // group norm keeps no moving statistics; a moving-statistics (frozen) step updates none
+  if (!c->gn && !c->bn_infer)
     HIPCALL(c, launch_moving_update(c->moving, c->moving + half, c->grads + c->n_train,
                                     c->grads + c->n_train + half, (int)half, c->cfg.bn_decay, s));
   if (c->n_flip) HIPCALL(c, launch_weight_flip_batched(c->dt, c->flip_jobs, c->n_flip, c->flip_total, s));

@@ -118,10 +118,10 @@ def model(mode, features, labels, config, params):
     ctx = get_context(config, params, mode=mode)
     assert features.shape[-1] == 3, 'features must be NHWC with 3 channels'
     # tf.contrib.layers.batch_norm(is_training=batch_norm_accumulate_statistics)
-    # (hierarchical.py:40-49,306-307). TRAIN always accumulates statistics here (train.py
-    # sets the flag; a frozen-statistics backward is not built); EVAL / PREDICT follow it.
-    infer = mode != ModeKeys.TRAIN and not bool(
-        getattr(params, 'batch_norm_accumulate_statistics', False))
+    # (hierarchical.py:40-49,306-307) in every mode: train.py sets the flag (train.py:46); a
+    # TRAIN step without it normalises with the moving statistics, differentiates through them
+    # as constants and leaves them unchanged (no UPDATE_OPS)
+    infer = not bool(getattr(params, 'batch_norm_accumulate_statistics', mode == ModeKeys.TRAIN))
     if getattr(ctx, 'bn_inference', False) != infer:
         ctx.set_bn_inference(infer)
     ctx.forward(features.contiguous())

@@ -32,7 +32,7 @@ def _rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def _native_step(cuda, cfg, params, data, dtype, lr=0.01, steps=1):
+def _native_step(cuda, cfg, params, data, dtype, lr=0.01, steps=1, frozen_bn=False):
     from input_pipelines import synthetic  # noqa: F401  (path check)
     from seg_hip import SegContext
     ctx = SegContext(depth=cfg.depth, pyramid=cfg.pyramid, height=cfg.height, width=cfg.width,
@@ -41,6 +41,8 @@ def _native_step(cuda, cfg, params, data, dtype, lr=0.01, steps=1):
                      fov_k=cfg.fov_k, fov_rate=cfg.fov_rate, upsampling=cfg.upsampling,
                      norm=cfg.norm, groups=cfg.groups)
     ctx.load_params(params)
+    if frozen_bn:
+        ctx.set_bn_inference(True)
     img = torch.as_tensor(data["images"]).to(cuda)
     px = torch.as_tensor(data["px"]).to(cuda) if cfg.nb_pp else None
     bb = torch.as_tensor(data["bbox"]).to(cuda) if cfg.nb_pb else None
@@ -428,3 +430,52 @@ def test_group_norm_layerwise(cuda, dtype):
                 checked += 1
     assert checked == 2 * (16 + 3)
     ctx.close()
+
+
+def test_frozen_bn_train_step_fp32(cuda):
+    """TRAIN without batch_norm_accumulate_statistics (hierarchical.py:306-307: is_training =
+    False): the forward normalises with the moving statistics, the backward differentiates
+    through them as constants (dy = gamma * invstd * dyhat, dgamma / dbeta as usual) and the
+    moving statistics stay unchanged. Losses, logits 1e-3, gradients conditioning-aware as in
+    test_train_step_fp32, SGDM arithmetic 1e-5, moving statistics bit-identical."""
+    from input_pipelines.synthetic import batch
+    cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="psp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=3).items()}
+    other = batch(99, cfg.nb, 0, 0, cfg.height, cfg.width)
+    net0 = OracleNet(cfg, params, dtype=torch.float64)
+    net0.forward(torch.as_tensor(other["images"]))
+    rng = np.random.default_rng(5)
+    for name, (m, v) in net0.batch_stats.items():   # moving statistics of another batch
+        params[f"{name}/BatchNorm/moving_mean"] = m.numpy().astype(np.float32)
+        params[f"{name}/BatchNorm/moving_variance"] = v.numpy().astype(np.float32)
+    for k in params:
+        if k.endswith("/gamma"):
+            params[k] = (1.0 + 0.1 * rng.standard_normal(params[k].shape)).astype(np.float32)
+        elif k.endswith("/beta"):
+            params[k] = (0.1 * rng.standard_normal(params[k].shape)).astype(np.float32)
+    data = batch(11, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
+    nat = _native_step(cuda, cfg, params, data, "fp32", frozen_bn=True)
+    ref = {}
+    for dt in (torch.float64, torch.float32):
+        net = OracleNet(cfg, params, dtype=dt)
+        net.bn_inference = True
+        ref[dt] = net.train_step(data["images"], data["px"], data.get("bbox"), data.get("tag"), lr=0.01)
+    L, low, g = ref[torch.float64][:3]
+    _, low32, g32 = ref[torch.float32][:3]
+    exp = [float(L["segmentation"]), float(L["l1_segmentation"])]
+    np.testing.assert_allclose(nat["losses"][:2], exp, rtol=1e-3)
+    refl = low["l1_logits"].detach().permute(0, 2, 3, 1).numpy()
+    gap = _rel(low32["l1_logits"].detach().permute(0, 2, 3, 1).numpy(), refl)
+    assert _rel(nat["logits"][..., :14], refl) < max(1e-3, 4 * gap)
+    errs = {k: _rel(nat["grads"][k], g[k].numpy().reshape(-1)) for k in g}
+    cond = {k: _rel(g32[k].numpy().reshape(-1), g[k].numpy().reshape(-1)) for k in g}
+    bad = [(errs[k], cond[k], k) for k in g
+           if errs[k] > (max(1e-3, 4 * cond[k]) if cond[k] < 1e-3 else max(5e-2, 2 * cond[k]))]
+    assert not bad, sorted(bad, reverse=True)[:10]
+    for k in g:
+        w = params[k].reshape(-1).astype(np.float64)
+        wd = cfg.weight_decay if k.endswith("/weights") else 0.0
+        assert _rel(nat["params"][k], w - 0.01 * (nat["grads"][k].astype(np.float64) + wd * w)) < 1e-5, k
+    for k in params:
+        if "moving" in k:
+            assert np.array_equal(nat["params"][k], params[k].reshape(-1)), k
