@@ -256,6 +256,21 @@ def main():
             gf = sum(v[0] for v in dil.values()); ms_ = sum(v[1] for v in dil.values())
             dilated["all"] = {"achieved": round(gf / ms_, 1), "frac": round(gf / ms_ / peak, 4),
                               "unit": "TFLOP/s"}
+        # SURVEY §8(d)'s recommended form beside the plain MFMA fraction: per launch the
+        # attainable time max(flops / P_mfma, compulsory bytes / BW_hbm) (short-K 1x1 layers and
+        # the small-channel weight gradients are HBM-bound at their arithmetic intensity), summed
+        # over the class and divided by its measured time; and the same sum over every profiled
+        # conv / BN launch against the step time
+        bound_ms = {}
+        for row in dump:
+            t_mfma = row["gflop"] / peak if row["cls"] <= 2 else 0.0      # GFLOP / (TFLOP/s) = ms
+            gb = row["gbytes"] if row["cls"] <= 2 else row["gflop"]     # BN classes: gflop = GB
+            bound_ms[row["cls"]] = bound_ms.get(row["cls"], 0.0) + max(t_mfma, gb / PEAK_HBM_TBS)
+        for c_, b_ms in bound_ms.items():
+            nm = CLS_NAMES[c_]
+            if nm in all_classes and all_classes[nm]["ms"] > 0:
+                all_classes[nm]["attainable_frac"] = round(b_ms / all_classes[nm]["ms"], 4)
+        step_bound = round(sum(bound_ms.values()) / (elapsed * 1e3 / args.steps), 4)
         names = dict(CLS_NAMES, **(CLS_NAMES_F32 if args.dtype == "fp32" else {}))
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -274,6 +289,8 @@ def main():
                     "classes_ms_per_step": {CLS_NAMES[c]: round(cls[c]["ms"], 2) for c in cls},
                     "classes": all_classes,
                     "dilated_3x3_encoder": dilated,
+                    "attainable_frac": all_classes.get(CLS_NAMES[dom], {}).get("attainable_frac"),
+                    "step_bound_frac": step_bound,
                     "max_layer": r["max_layer"]}
         ctx.profile(False)
 

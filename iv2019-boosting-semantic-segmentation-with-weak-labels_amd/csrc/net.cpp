@@ -412,9 +412,13 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
 }
 
 // concurrent = the weight gradient runs on the side stream beside the dgrad -> BN chain:
-// target ~128 workgroups (half the CUs, the chain keeps the other half: 90.4 -> 92.9 img/s
+// at most ~128 workgroups (half the CUs, the chain keeps the other half: 90.4 -> 92.9 img/s
 // on C2 against 512, and half the split-K slab traffic); alone (profiled, single stream,
-// seg_op_*): ~2 waves of the 256 CUs.
+// seg_op_*): at most one wave of the 256 CUs (one workgroup per CU, LDS-bound). The weight-
+// gradient kernels run one workgroup per CU, so a launch of 256 + a few workgroups pays a
+// whole second wave for the few: tools/wgrad_sweep.py PP_ONLY=1 on the C2 shapes, e.g. block3
+// 3x3 (9 tiles) 24 splits 188 us, 32 splits (288 workgroups) 266 us; block3 1x1 (4 tiles) 64
+// splits 97 us against the former 2-wave 128 splits 121 us.
 int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false, int k = 0) {
   if (!ci) ci = L.ci;   // 16 for the space-to-depth stem
   if (!k) k = L.k;      // 4 for the space-to-depth stem
@@ -423,10 +427,11 @@ int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false, int k = 0)
   long P = (long)L.N * L.Ho * L.Wo;
   if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, k * k * ci, P, &BM, &BN);
   long tiles = (long)((L.co_pad + BM - 1) / BM) * ((k * k * ci + BN - 1) / BN);
-  // each split >= 32 K-steps of 64 pixels
-  const long target = concurrent ? 128 : 512;
+  // workgroups = tiles x splits <= one wave of the CUs the launch may use; each split >= 32
+  // K-steps of 64 pixels beside the dgrad chain, >= 16 alone
+  const long target = concurrent ? 128 : 256;
   long s = std::max<long>(1, target / std::max<long>(tiles, 1));
-  long maxs = std::max<long>(1, P / 2048);
+  long maxs = std::max<long>(1, P / (concurrent ? 2048 : 1024));
   s = std::min(s, maxs);
   return (int)std::min<long>(s, 256);
 }

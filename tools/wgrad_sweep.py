@@ -21,7 +21,13 @@ SHAPES = {  # N, H, W, Ci, Co, k, stride, rate
     "b2c3": (4, 128, 256, 128, 512, 1, 1, 1),
     "b3c2": (4, 128, 256, 256, 256, 3, 1, 2),
     "b3c3": (4, 128, 256, 256, 1024, 1, 1, 1),
+    "b3c1": (4, 128, 256, 1024, 256, 1, 1, 1),
+    "b4c1": (4, 128, 256, 2048, 512, 1, 1, 1),
+    "b4c3": (4, 128, 256, 512, 2048, 1, 1, 1),
+    "b4c2": (4, 128, 256, 512, 512, 3, 1, 4),
+    "head1": (4, 128, 256, 256, 256, 1, 1, 1),
 }
+PP_ONLY = os.environ.get("PP_ONLY") == "1"   # 256 x 256 tiles (the ping-pong kernel) only
 vp, ip, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
 LIB.seg_op_conv_wgrad_cfg.argtypes = [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip,
                                       ip, vp, vp, i64, ip, ip, ip, vp]
@@ -38,13 +44,13 @@ for name in layers:
     P, ncol = N * H * W, k * k * Ci
     fl = 2.0 * P * Co * ncol
     res = []
-    for bm in (64, 128, 256):
+    for bm in ((256,) if PP_ONLY else (64, 128, 256)):
         if bm > 64 and Co <= bm // 2:
             continue
-        for bn in (64, 128, 256):
+        for bn in ((256,) if PP_ONLY else (64, 128, 256)):
             if bn > 64 and ncol <= bn // 2:
                 continue
-            for sp in (32, 64, 128, 256, 512):
+            for sp in ((4, 8, 16, 24, 32, 48, 64, 96, 128) if PP_ONLY else (32, 64, 128, 256, 512)):
                 if sp > max(1, P // 1024) or sp * Co * ncol * 4 > ws.numel():
                     continue
                 def run():
@@ -64,4 +70,6 @@ for name in layers:
     res.sort()
     print(f"{name} (Co {Co}, Ncol {ncol}, P {P}): best " +
           ", ".join(f"{bm}x{bn}/s{sp} {ms*1e3:.1f}us {fl/ms/1e9:.0f}TF/s" for ms, bm, bn, sp in res[:4]))
+    if PP_ONLY:
+        print("   all: " + ", ".join(f"s{sp} {ms*1e3:.0f}" for ms, bm, bn, sp in sorted(res, key=lambda t: t[3])))
     sys.stdout.flush()
