@@ -45,6 +45,8 @@ torch.cuda.synchronize()
 rows = ctx.profile_dump()
 CLS = ["fwd", "dgrad", "wgrad", "bn_apply", "bn_bwd_reduce", "bn_bwd_apply"]
 tot = collections.defaultdict(lambda: [0.0, 0.0, 0])
+att = collections.defaultdict(float)
+fam_att = collections.defaultdict(float)
 out = []
 for r in rows:
     c = r["cls"]
@@ -58,20 +60,26 @@ for r in rows:
         rate = r["gflop"] / r["ms"]            # TB/s (gflop field = GB for BN classes)
         ideal = r["gflop"] / 6.0
         unit = "TB/s"
+    if c < 3:   # attainable: max(flops / 2.5 PF, compulsory bytes / 6.3 TB/s achievable)
+        att[CLS[c]] += max(r["gflop"] / 2500.0, r.get("gbytes", 0.0) / 6.3)
+        fam_att[(CLS[c], r["ci"], r["co"], r["k"], r["ho"])] += max(r["gflop"] / 2500.0, r.get("gbytes", 0.0) / 6.3)
     out.append((r["ms"] - ideal, CLS[c], r["name"], r["ci"], r["co"], r["k"], r["rate"], r["ho"], r["wo"], r["ms"], rate, unit,
                 r.get("gbytes", 0.0) / r["ms"] if c < 3 else rate))
 print(f"{name}: class totals")
 for k in CLS:
     ms, gf, n = tot[k]
     u = "TF/s" if k in ("fwd", "dgrad", "wgrad") else "TB/s"
-    print(f"  {k:14s} {n:4d} launches {ms:8.3f} ms  {gf / max(ms, 1e-9):8.1f} {u}")
+    extra = f"  attainable {att[k]:7.3f} ms ({att[k] / max(ms, 1e-9):.2f})" if k in att else ""
+    print(f"  {k:14s} {n:4d} launches {ms:8.3f} ms  {gf / max(ms, 1e-9):8.1f} {u}{extra}")
 fam = collections.defaultdict(lambda: [0.0, 0.0, 0])
 for lost, c, nm, ci, co, k, rt, ho, wo, ms, rate, unit, tbs in out:
     key = (c, ci, co, k, ho)
     fam[key][0] += ms; fam[key][1] += lost; fam[key][2] += 1
 print("\nfamilies (class ci co k Ho): launches, ms, ms above the reference rate")
 for key, (ms, lost, n) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
-    print(f"  {key[0]:13s} {key[1]:5d} {key[2]:5d} k{key[3]} {key[4]:4d}  {n:3d}  {ms:7.3f} ms  {lost:7.3f} ms")
+    a = fam_att.get(key)
+    at = f"  attainable {a:7.3f} ms ({a / ms:.2f})" if a else ""
+    print(f"  {key[0]:13s} {key[1]:5d} {key[2]:5d} k{key[3]} {key[4]:4d}  {n:3d}  {ms:7.3f} ms  {lost:7.3f} ms{at}")
 print("\nlaunches by time above the reference rate (ms lost, class, layer, ci co k rate HoxWo, ms, rate, compulsory TB/s)")
 for lost, c, nm, ci, co, k, rt, ho, wo, ms, rate, unit, tbs in sorted(out, reverse=True)[:70]:
     print(f"{lost:7.3f} {c:13s} {nm[-58:]:58s} {ci:5d} {co:5d} {k} r{rt:<2d} {ho}x{wo} {ms:7.3f} ms {rate:7.1f} {unit} {tbs:5.2f} TB/s")
