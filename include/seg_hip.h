@@ -219,7 +219,8 @@ int seg_op_conv_fwd(int dtype, const void* x, int N, int H, int W, int C, int ld
                     const void* w, int Co, int k, int stride, int rate, int explicit_pad,
                     void* y, int ldy, float* stats, void* stream);
 /* rows per BN-statistics partial written by seg_op_conv_fwd for this shape (128 or 256) */
-int seg_op_conv_stat_rows(int dtype, int C, int ldx, int Co, int ldy, int k);
+int seg_op_conv_stat_rows(int dtype, int N, int H, int W, int C, int ldx, int Co, int ldy, int k,
+                          int stride, int rate, int explicit_pad);
 int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
                       const void* w, int Ci, int k, int stride, int rate, int explicit_pad,
                       int H, int W, void* dx, int lddx, void* stream);

@@ -442,6 +442,286 @@ hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ======================================================================================
+// Small-channel 3x3 convolutions (stride 1, dilation 1, C in {64, 128}, Co in {64, 128}): the
+// v2 gather re-reads every input pixel once per tap (9 L2 -> LDS passes over the same rows),
+// which bounds those layers at 0.15-0.25 of their attainable time (profiles/r02_step_report).
+// Here a tile is 8 output rows x 32 pixels of one image; its input patch (10 x 34 pixels x 64
+// channels = 43.5 KB per channel chunk, XOR-swizzled 128-B rows) is staged in LDS once per
+// chunk by LDS-DMA, and the nine taps read their A fragments from the patch at shifted rows
+// (16 consecutive output pixels -> 16 consecutive patch rows: the conflict-free ds_read_b128
+// pattern of the v2 kernel). Weights stream through a 3-stage ring per K-step (tap-minor);
+// chunk 1's patch goes into the second patch buffer one 64-row piece per K-step during chunk
+// 0, issued before that K-step's weights so every counted vmcnt stays exact. Epilogue as v2
+// (BN partial statistics per 256-row tile, fp32 staging, 16-B stores) with the tile's rows
+// mapped back to pixels.
+// ======================================================================================
+constexpr int PT_H = 8, PT_W = 32;            // output tile
+constexpr int PP_H = PT_H + 2, PP_W = PT_W + 2;  // input patch (3x3, dilation 1)
+constexpr int PP_ROWS = 384;                  // 340 patch pixels padded to 6 x 64 DMA rows
+constexpr int PP_BYTES = PP_ROWS * 128;
+
+// NPB patch buffers (2: chunk 1 streamed during chunk 0; 1: reloaded between chunks), NST weight
+// stages, OCC workgroups per CU (2 when the LDS fits 80 KB: the other workgroup hides this one's
+// barrier and fragment-read latency)
+template <typename E, int BN, int WMW, int WNW, int NPB, int NST, int OCC>
+__global__ __launch_bounds__(V2_THREADS, 2 * OCC) void conv_nt_patch_kernel(ConvArgs a) {   // (waves per SIMD)
+  typedef typename Half<E>::V V;
+  const E* zero = (const E*)g_zero16;
+  constexpr int BM = PT_H * PT_W;
+  constexpr int WM = BM / WMW, WN = BN / WNW;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int BI = BN * 8 / V2_THREADS;     // weight glds per lane per K-step
+  constexpr int BSTAGE = BN * 128;
+  constexpr int EPI_COLS = 64, EPI_LD = EPI_COLS + 4;
+  static_assert(WMW * WNW == 8 && (WM % PT_W == 0 || PT_W % WM == 0), "wave rows");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const patch = smem;                     // two chunk buffers
+  char* const bring = smem + NPB * PP_BYTES;    // NST weight stages
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int tiles_x = a.Wo / PT_W, tiles_y = a.Ho / PT_H;
+  const int ntiles = a.Co / BN;   // output-channel tiles (n fastest: they share the patch in L2)
+  const int nwg = a.N * tiles_y * tiles_x * ntiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int n0 = (wg % ntiles) * BN;
+  const int pt = wg / ntiles;     // pixel tile = BN-statistics partial index
+  const int tx0 = (pt % tiles_x) * PT_W;
+  const int ty0 = ((pt / tiles_x) % tiles_y) * PT_H;
+  const int nimg = pt / (tiles_x * tiles_y);
+  const int nch = a.C / BK;
+  const int nk = 9 * nch;
+  const E* X = (const E*)a.x;
+  const E* Wt = (const E*)a.w;
+  const int pc = lane & 7;
+
+  // patch piece i (64 rows) of channel chunk c into buffer c & 1
+  auto issue_piece = [&](int c, int i) {
+    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+    const int py = row / PP_W, px = row - py * PP_W;
+    const int hi = ty0 - a.pad_h + py, wi = tx0 - a.pad_w + px;
+    const bool ok = row < PP_H * PP_W && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+    const size_t off = ((size_t)((long)nimg * a.H + hi) * a.W + wi) * a.ldx + c * BK + swz(row, pc) * 8;
+    glds16(ok ? (const void*)(X + off) : (const void*)zero, patch + (c % NPB) * PP_BYTES + (i * 8 + wave) * 1024);
+  };
+  auto issue_b = [&](int kb) {
+    const int tap = kb % 9, c = kb / 9;
+    const int k0 = tap * a.C + c * BK;
+    char* sB = bring + (kb % NST) * BSTAGE;
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = (i * 8 + wave) * 8 + (lane >> 3);
+      glds16(Wt + (size_t)(n0 + row) * a.ldw + k0 + swz(row, pc) * 8, sB + (i * 8 + wave) * 1024);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  // A fragment row i of this wave -> (output row, column) inside the tile
+  auto frag_pix = [&](int i, int& ty, int& tx) {
+    const int r = wm * WM + i * 16;
+    ty = r / PT_W;
+    tx = r - ty * PT_W;
+  };
+
+  // prologue: patch chunk 0 (6 pieces), weights of K-steps 0 and 1
+#pragma unroll
+  for (int i = 0; i < 6; ++i) issue_piece(0, i);
+  issue_b(0);
+  if (NST == 3 && nk > 1) issue_b(1);
+  for (int kb = 0; kb < nk; ++kb) {
+    // wait for B(kb) (and everything before it: the current chunk's patch); after it were
+    // issued: iteration kb-1's patch piece (if any) and B(kb+1) (3 stages)
+    const bool piece_prev = NPB == 2 && kb >= 1 && nch == 2 && kb - 1 < 6;
+    const bool b_next = NST == 3 && kb + 1 < nk;
+    if (b_next && piece_prev) wait_vmcnt<BI + 1>();
+    else if (b_next) wait_vmcnt<BI>();
+    else if (piece_prev) wait_vmcnt<1>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();   // every lane's DMA for kb landed; stage (kb - 1) % NST is free
+    if (NPB == 1 && kb > 0 && kb % 9 == 0) {   // one patch buffer: reload it for the next chunk
+      if (NST == 2 && kb + 1 < nk) issue_b(kb + 1);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) issue_piece(kb / 9, i);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+    } else if (NST == 2 && kb + 1 < nk) {
+      issue_b(kb + 1);
+    }
+    if (NPB == 2 && nch == 2 && kb < 6) issue_piece(1, kb);
+    if (NST == 3 && kb + 2 < nk) issue_b(kb + 2);
+    const int tap = kb % 9, c = kb / 9;
+    const int kh = tap / 3, kw = tap - kh * 3;
+    const char* P = patch + (c % NPB) * PP_BYTES;
+    const char* B = bring + (kb % NST) * BSTAGE;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      V af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        int ty, tx;
+        frag_pix(i, ty, tx);
+        const int prow = (ty + kh) * PP_W + tx + kw + lr;
+        af[i] = *(const V*)(P + prow * 128 + swz(prow, lq + 4 * s2) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * WN + j * 16 + lr;
+        bfr[j] = *(const V*)(B + row * 128 + swz(row, lq + 4 * s2) * 16);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = Half<E>::mma(af[i], bfr[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // ---- epilogue (every tile is full: Ho % 8 == 0, Wo % 32 == 0) ----
+  auto row_of = [&](int i, int k) { return wm * WM + i * 16 + lq * 4 + k; };
+  auto col_of = [&](int j) { return wn * WN + j * 16 + lr; };
+  if (a.stats) {
+    // as conv_nt_v2_kernel's full-tile path: per lane (sum, M2) of its 4 * FM rows, Chan
+    // merges over the lane groups (shfl 16, 32) and the WMW waves (LDS), fixed order
+    float2* red2 = (float2*)smem;
+    constexpr float NL = (float)(4 * FM);
+    float sj[FN], mj[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float x = acc[i][j][k];
+          sm += x;
+          sq = __builtin_fmaf(x, x, sq);
+        }
+      sj[j] = sm;
+      mj[j] = fmaxf(sq - sm * sm * (1.f / NL), 0.f);
+    }
+    float n = NL;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
+        const float d = (s2 - sj[j]) / n;
+        mj[j] = mj[j] + m2 + d * d * (0.5f * n);
+        sj[j] += s2;
+      }
+      n *= 2.f;
+    }
+    if (lq == 0)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
+    __syncthreads();
+    if (wm == 0 && lq == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = col_of(j);
+        float2 t = red2[c];
+        float nt = (float)WM;
+#pragma unroll
+        for (int w = 1; w < WMW; ++w) {
+          const float2 u = red2[w * BN + c];
+          const float d = u.x / (float)WM - t.x / nt;
+          t.y = t.y + u.y + d * d * (nt * (float)WM / (nt + (float)WM));
+          t.x += u.x;
+          nt += (float)WM;
+        }
+        *(float2*)(a.stats + 2 * ((size_t)pt * a.Co + n0 + c)) = t;
+      }
+    }
+    __syncthreads();
+  }
+  float* stage = (float*)smem;
+  E* Y = (E*)a.y;
+  const E* R1 = (const E*)a.r;
+  const E* R2 = (const E*)a.r2;
+  const int s_rl = tid >> 3, s_cc = tid & 7;
+#pragma unroll
+  for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
+    const int cbase = pass * EPI_COLS;
+    if (wn * WN + WN > cbase && wn * WN < cbase + EPI_COLS) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = col_of(j);
+        if (col >= cbase && col < cbase + EPI_COLS) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = acc[i][j][k];
+        }
+      }
+    }
+    __syncthreads();
+    const int n = n0 + cbase + s_cc * 8;
+    {
+#pragma unroll
+      for (int rr = 0; rr < BM / 64; ++rr) {
+        const int row = s_rl + 64 * rr;
+        const int ty = row / PT_W, tx = row - ty * PT_W;
+        const long m = ((long)nimg * a.Ho + ty0 + ty) * a.Wo + tx0 + tx;
+        const float* sp = stage + row * EPI_LD + s_cc * 8;
+        const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
+        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        if (R1) {
+          float u[8];
+          Vec8<E>::load(R1 + (size_t)m * a.ldr + n, u);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += u[e];
+        }
+        if (R2) {
+          float u[8];
+          Vec8<E>::load(R2 + (size_t)m * a.ldr2 + n, u);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += u[e];
+        }
+        store8_nt(Y + (size_t)m * a.ldy + n, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <typename E, int BN, int WMW, int WNW, int NPB, int NST, int OCC>
+hipError_t patch_launch(const ConvArgs& a, hipStream_t s) {
+  constexpr int LDS = NPB * PP_BYTES + NST * BN * 128;
+  static_assert(LDS * OCC <= 160 * 1024 && LDS >= 256 * (64 + 4) * 4, "LDS budget / epilogue staging");
+  auto kern = conv_nt_patch_kernel<E, BN, WMW, WNW, NPB, NST, OCC>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nwg = a.N * (a.Ho / PT_H) * (a.Wo / PT_W) * (a.Co / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(V2_THREADS), LDS, s, a);
+  return hipGetLastError();
+}
+
+// the patch kernel's shapes (see above); SEG_PATCH=0 turns it off (A/B)
+bool conv_nt_patch_ok(const ConvArgs& a) {
+  static const bool on = [] { const char* e = getenv("SEG_PATCH"); return !(e && e[0] == '0'); }();
+  return on && !a.tap8 && a.st == 1 && a.sf == 1 && a.dil == 1 && a.KH == 3 && a.KW == 3 &&
+         (a.C == 64 || a.C == 128) && (a.Co == 64 || a.Co == 128) && a.ldw == 9 * a.C &&
+         a.H == a.Ho && a.W == a.Wo && a.Ho % PT_H == 0 && a.Wo % PT_W == 0 &&
+         a.pad_h >= 0 && a.pad_h <= 2 && a.pad_w >= 0 && a.pad_w <= 2 &&
+         a.ldx % 8 == 0 && a.ldy % 8 == 0;
+}
+
 }  // namespace
 
 // bf16 fast path: C % 64 == 0, ld/co multiples of 8; stats tiles are 256 rows
@@ -467,11 +747,19 @@ static bool v2_small_tile(const ConvArgs& a) { return a.Co <= 64; }
 int conv_nt_v2_rows(const ConvArgs& a) {
   // the ping-pong kernel writes one partial per wave row (128 rows), the v2 kernels per tile
   if (a.Co > 128 && !a.r && !a.r2 && conv_nt_pp_ok(a)) return 128;
+  if (conv_nt_patch_ok(a)) return 256;
   return v2_small_tile(a) ? 128 : 256;
 }
 
 template <typename E, int ST>
 hipError_t v2_dispatch(int dtype, const ConvArgs& a, hipStream_t s) {
+  if (ST == 1 && conv_nt_patch_ok(a)) {
+    // 64-channel output tiles with one patch buffer fit 72 KB and 110 VGPRs: two workgroups
+    // per CU hide each other's barrier and fragment-read latency (a 128-channel tile at two
+    // per CU needs <= 128 VGPRs and spilled); Co = 128 runs as two such tiles per patch, the
+    // 128-channel input as two chunks with the patch reloaded between them
+    return patch_launch<E, 64, 8, 1, 1, 3, 2>(a, s);
+  }
   if (a.Co > 128) {
     if (conv_nt_pp_ok(a)) return launch_conv_nt_pp(dtype, a, s);
     return v2_launch<E, 256, 4, 2, 2, ST>(a, s);

@@ -1896,9 +1896,14 @@ int seg_op_conv_fwd(int dtype, const void* x, int N, int H, int W, int C, int ld
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_fwd");
 }
 
-int seg_op_conv_stat_rows(int dtype, int C, int ldx, int Co, int ldy, int k) {
+int seg_op_conv_stat_rows(int dtype, int N, int H, int W, int C, int ldx, int Co, int ldy, int k,
+                          int stride, int rate, int explicit_pad) {
+  int Ho, Wo, ph, pw;   // the ConvArgs seg_op_conv_fwd builds (the kernel choice is shape-dependent)
+  op_geom(H, W, k, stride, rate, explicit_pad, &Ho, &Wo, &ph, &pw);
   ConvArgs a{};
-  a.C = C; a.ldx = ldx; a.Co = Co; a.ldy = ldy; a.ldw = 8; a.st = 1; a.KH = a.KW = k;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.ldx = ldx; a.ldw = k * k * C; a.Ho = Ho; a.Wo = Wo;
+  a.Co = Co; a.ldy = ldy; a.KH = a.KW = k; a.sf = stride; a.st = 1; a.pad_h = ph; a.pad_w = pw;
+  a.dil = rate;
   return conv_nt_stat_rows(dt_of(dtype), 0, a);
 }
 

@@ -96,7 +96,7 @@ def _load():
                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                   ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ip]),
         "seg_op_conv_fwd": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, vp, ip, vp, vp]),
-        "seg_op_conv_stat_rows": (ip, [ip, ip, ip, ip, ip, ip]),
+        "seg_op_conv_stat_rows": (ip, [ip] * 12),
         "seg_op_conv_dgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, vp,
                                    ip, vp]),
         "seg_op_conv_wgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, ip,

@@ -22,6 +22,10 @@ CASES = [
     (2, 9, 10, 256, 3, 1, 1, 1, False),       # l2 human logits
     (1, 6, 6, 1280, 256, 1, 1, 1, False),     # PSP final (C=1280)
     (2, 15, 21, 256, 512, 1, 1, 1, False),    # short K, wide N: 128-row tiles, 2 per CU
+    # small-channel 3x3 patch kernel (8 x 32 pixel tiles, input patch staged once per chunk)
+    (2, 16, 64, 64, 64, 3, 1, 1, False),      # one 64-channel chunk, Co 64
+    (1, 24, 96, 128, 128, 3, 1, 1, False),    # two chunks (second patch streamed), Co 128
+    (1, 8, 32, 128, 64, 3, 1, 1, False),      # two chunks, Co 64 (its dgrad: one chunk, Co 128)
 ]
 
 
@@ -92,7 +96,7 @@ def test_conv_fwd(cuda, dtype, case):
     tol = TOL[dtype]
     assert _rel(y, ref) < tol
     # BN partial statistics: merge (sum, M2 about the tile mean) and compare
-    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], Ci, Ci, Co, Co, k)
+    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], N, H, W, Ci, Ci, Co, Co, k, s, r, int(ep))
     nt = (M + tr - 1) // tr
     st = stats.cpu().numpy().astype(np.float64)[:nt]
     cnt = np.minimum(tr, M - np.arange(nt) * tr).astype(np.float64)

@@ -90,9 +90,14 @@ C2_LAYERS = [
     ("aspp_conv_r18", 4, 128, 256, 256, 256, 3, 1, 18, False),
     ("block1_conv2_s2", 4, 256, 512, 64, 64, 3, 2, 1, True),
     ("block2_conv1_co128", 4, 128, 256, 256, 128, 1, 1, 1, False),
+    # the small-channel 3x3 patch kernel (conv_v2.hip conv_nt_patch_kernel): forward and the
+    # stride-1 data gradient of block1 / block2 conv2
+    ("block1_conv2_c64", 4, 256, 512, 64, 64, 3, 1, 1, False),
+    ("block2_conv2_c128", 4, 128, 256, 128, 128, 3, 1, 1, False),
     ("l1_logits_co14", 4, 128, 256, 256, 14, 1, 1, 1, False),
 ]
-LAYER_DTYPES = [(c, "bf16") for c in C2_LAYERS] + [(C2_LAYERS[0], "fp16"), (C2_LAYERS[2], "fp16")]
+LAYER_DTYPES = [(c, "bf16") for c in C2_LAYERS] + [(C2_LAYERS[0], "fp16"), (C2_LAYERS[2], "fp16"),
+                                                    (C2_LAYERS[9], "fp16")]
 
 
 def _operands(case, dtype, seed):
@@ -127,7 +132,7 @@ def test_conv_c2_layer(cuda, case, dtype):
     torch.cuda.synchronize()
     refd = ref.to(cuda)
     _elementwise(yd, refd, 2 * ULP[dtype], 1e-3, f"{name} fwd")
-    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], Ci, Ci, Co, Co, k)
+    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], N, H, W, Ci, Ci, Co, Co, k, s, r, int(ep))
     nt = (M + tr - 1) // tr
     sp = stats[:nt].double()
     cnt = torch.clamp(M - torch.arange(nt, device=cuda) * tr, max=tr).double()
