@@ -1,5 +1,5 @@
 set -e
-tag=r02v14
+tag=${TAG:-r02v14}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
