@@ -464,6 +464,127 @@ constexpr int PP_BYTES = PP_ROWS * 128;
 // NPB patch buffers (2: chunk 1 streamed during chunk 0; 1: reloaded between chunks), NST weight
 // stages, OCC workgroups per CU (2 when the LDS fits 80 KB: the other workgroup hides this one's
 // barrier and fragment-read latency)
+// epilogue of the patch kernels (every tile is full: Ho % 8 == 0, Wo % 32 == 0): BN partial
+// statistics of the 256-row tile (index pt), fp32 staging through LDS, 16-B stores of the
+// tile's pixels (+ residuals)
+template <typename E, int BN, int WMW, int WNW>
+__device__ __forceinline__ void patch_epilogue(const ConvArgs& a, f32x4_t (&acc)[(PT_H * PT_W / WMW) / 16][(BN / WNW) / 16],
+                                               char* smem, int pt, int n0, int nimg, int ty0, int tx0) {
+  constexpr int BM = PT_H * PT_W;
+  constexpr int WM = BM / WMW, WN = BN / WNW;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int EPI_COLS = 64, EPI_LD = EPI_COLS + 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int lr = lane & 15, lq = lane >> 4;
+  auto row_of = [&](int i, int k) { return wm * WM + i * 16 + lq * 4 + k; };
+  auto col_of = [&](int j) { return wn * WN + j * 16 + lr; };
+  if (a.stats) {
+    // as conv_nt_v2_kernel's full-tile path: per lane (sum, M2) of its 4 * FM rows, Chan
+    // merges over the lane groups (shfl 16, 32) and the WMW waves (LDS), fixed order
+    float2* red2 = (float2*)smem;
+    constexpr float NL = (float)(4 * FM);
+    float sj[FN], mj[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float x = acc[i][j][k];
+          sm += x;
+          sq = __builtin_fmaf(x, x, sq);
+        }
+      sj[j] = sm;
+      mj[j] = fmaxf(sq - sm * sm * (1.f / NL), 0.f);
+    }
+    float n = NL;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
+        const float d = (s2 - sj[j]) / n;
+        mj[j] = mj[j] + m2 + d * d * (0.5f * n);
+        sj[j] += s2;
+      }
+      n *= 2.f;
+    }
+    if (lq == 0)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
+    __syncthreads();
+    if (wm == 0 && lq == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = col_of(j);
+        float2 t = red2[c];
+        float nt = (float)WM;
+#pragma unroll
+        for (int w = 1; w < WMW; ++w) {
+          const float2 u = red2[w * BN + c];
+          const float d = u.x / (float)WM - t.x / nt;
+          t.y = t.y + u.y + d * d * (nt * (float)WM / (nt + (float)WM));
+          t.x += u.x;
+          nt += (float)WM;
+        }
+        *(float2*)(a.stats + 2 * ((size_t)pt * a.Co + n0 + c)) = t;
+      }
+    }
+    __syncthreads();
+  }
+  float* stage = (float*)smem;
+  E* Y = (E*)a.y;
+  const E* R1 = (const E*)a.r;
+  const E* R2 = (const E*)a.r2;
+  const int s_rl = tid >> 3, s_cc = tid & 7;
+#pragma unroll
+  for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
+    const int cbase = pass * EPI_COLS;
+    if (wn * WN + WN > cbase && wn * WN < cbase + EPI_COLS) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = col_of(j);
+        if (col >= cbase && col < cbase + EPI_COLS) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = acc[i][j][k];
+        }
+      }
+    }
+    __syncthreads();
+    const int n = n0 + cbase + s_cc * 8;
+    {
+#pragma unroll
+      for (int rr = 0; rr < BM / 64; ++rr) {
+        const int row = s_rl + 64 * rr;
+        const int ty = row / PT_W, tx = row - ty * PT_W;
+        const long m = ((long)nimg * a.Ho + ty0 + ty) * a.Wo + tx0 + tx;
+        const float* sp = stage + row * EPI_LD + s_cc * 8;
+        const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
+        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        if (R1) {
+          float u[8];
+          Vec8<E>::load(R1 + (size_t)m * a.ldr + n, u);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += u[e];
+        }
+        if (R2) {
+          float u[8];
+          Vec8<E>::load(R2 + (size_t)m * a.ldr2 + n, u);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += u[e];
+        }
+        store8_nt(Y + (size_t)m * a.ldy + n, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <typename E, int BN, int WMW, int WNW, int NPB, int NST, int OCC>
 __global__ __launch_bounds__(V2_THREADS, 2 * OCC) void conv_nt_patch_kernel(ConvArgs a) {   // (waves per SIMD)
   typedef typename Half<E>::V V;
@@ -473,10 +594,9 @@ __global__ __launch_bounds__(V2_THREADS, 2 * OCC) void conv_nt_patch_kernel(Conv
   constexpr int FM = WM / 16, FN = WN / 16;
   constexpr int BI = BN * 8 / V2_THREADS;     // weight glds per lane per K-step
   constexpr int BSTAGE = BN * 128;
-  constexpr int EPI_COLS = 64, EPI_LD = EPI_COLS + 4;
   static_assert(WMW * WNW == 8 && (WM % PT_W == 0 || PT_W % WM == 0), "wave rows");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const patch = smem;                     // two chunk buffers
+  char* const patch = smem;                     // NPB chunk buffers
   char* const bring = smem + NPB * PP_BYTES;    // NST weight stages
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -588,112 +708,94 @@ __global__ __launch_bounds__(V2_THREADS, 2 * OCC) void conv_nt_patch_kernel(Conv
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  // ---- epilogue (every tile is full: Ho % 8 == 0, Wo % 32 == 0) ----
-  auto row_of = [&](int i, int k) { return wm * WM + i * 16 + lq * 4 + k; };
-  auto col_of = [&](int j) { return wn * WN + j * 16 + lr; };
-  if (a.stats) {
-    // as conv_nt_v2_kernel's full-tile path: per lane (sum, M2) of its 4 * FM rows, Chan
-    // merges over the lane groups (shfl 16, 32) and the WMW waves (LDS), fixed order
-    float2* red2 = (float2*)smem;
-    constexpr float NL = (float)(4 * FM);
-    float sj[FN], mj[FN];
+  patch_epilogue<E, BN, WMW, WNW>(a, acc, smem, pt, n0, nimg, ty0, tx0);
+}
+
+// The space-to-depth stem (tap mode: a 4 x 4 VALID conv over 16-channel s2d pixels, K = 256)
+// on the same tiles: the tile's 11 x 35-pixel s2d patch (32-B pixels, 12.3 KB; the 16-B halves
+// swapped on every other group of 8 pixels so 16 consecutive pixels hit distinct banks) and all
+// 256 K-columns of the 64 output channels' weights (32 KB) are staged once; a K-step is 4 taps x 2
+// chunks, each lane's chunk addressed at its tap's shifted patch pixel. (The v2 tap-mode gather
+// re-read every s2d pixel once per tap: 16 L2 -> LDS passes.)
+constexpr int PS_H = PT_H + 3, PS_W = PT_W + 3;   // 4 x 4 taps
+constexpr int PS_PIX = 512;                       // 385 patch pixels padded to 2 DMA rounds
+
+template <typename E>
+__global__ __launch_bounds__(V2_THREADS, 4) void conv_nt_patch_s2d_kernel(ConvArgs a) {
+  typedef typename Half<E>::V V;
+  constexpr int BN = 64, WMW = 8, WNW = 1;
+  constexpr int WM = PT_H * PT_W / WMW, WN = BN / WNW;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  const E* zero = (const E*)g_zero16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const patch = smem;                      // PS_PIX x 32 B
+  char* const wb = smem + PS_PIX * 32;           // 4 K-steps x 64 rows x 128 B
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int tiles_x = a.Wo / PT_W, tiles_y = a.Ho / PT_H;
+  const int nwg = a.N * tiles_y * tiles_x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int pt = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tx0 = (pt % tiles_x) * PT_W;
+  const int ty0 = ((pt / tiles_x) % tiles_y) * PT_H;
+  const int nimg = pt / (tiles_x * tiles_y);
+  const E* X = (const E*)a.x;
+  const E* Wt = (const E*)a.w;
+  auto sw = [](int p) { return (p >> 3) & 1; };   // 16-B half swap per 8-pixel group
+  // patch: 2 rounds of 512 x 16 B (pixel p = 256 i + tid / 2, physical half tid & 1)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float sm = 0.f, sq = 0.f;
+  for (int i = 0; i < 2; ++i) {
+    const int p = (i * 8 + wave) * 32 + (lane >> 1);
+    const int py = p / PS_W, px = p - py * PS_W;
+    const bool ok = p < PS_H * PS_W;   // VALID: inside the (Ho + 3) x (Wo + 3) s2d image
+    const size_t off = ((size_t)((long)nimg * a.H + ty0 + py) * a.W + tx0 + px) * 16 + ((lane & 1) ^ sw(p)) * 8;
+    glds16(ok ? (const void*)(X + off) : (const void*)zero, patch + (i * 8 + wave) * 1024);
+  }
+  // weights: 4 K-steps x 64 rows of 128 B (rows swizzled as the v2 B operand)
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    const int row = wave * 8 + (lane >> 3);
+    glds16(Wt + (size_t)row * a.ldw + kb * BK + swz(row, lane & 7) * 8, wb + kb * 8192 + wave * 1024);
+  }
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    const char* B = wb + kb * 8192;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int cc = lq + 4 * s2;                 // this lane's 16-B chunk of the K-step
+      const int tap = kb * 4 + (cc >> 1), hf = cc & 1;
+      const int kh = tap >> 2, kw = tap & 3;
+      V af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * WM + i * 16;
+        const int ty = r / PT_W, tx = r - ty * PT_W;
+        const int p = (ty + kh) * PS_W + tx + kw + lr;
+        af[i] = *(const V*)(patch + p * 32 + ((hf ^ sw(p)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = j * 16 + lr;
+        bfr[j] = *(const V*)(B + row * 128 + swz(row, cc) * 16);
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float x = acc[i][j][k];
-          sm += x;
-          sq = __builtin_fmaf(x, x, sq);
-        }
-      sj[j] = sm;
-      mj[j] = fmaxf(sq - sm * sm * (1.f / NL), 0.f);
+        for (int j = 0; j < FN; ++j) acc[i][j] = Half<E>::mma(af[i], bfr[j], acc[i][j]);
     }
-    float n = NL;
-#pragma unroll
-    for (int o = 16; o <= 32; o <<= 1) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const float s2 = __shfl_xor(sj[j], o, 64), m2 = __shfl_xor(mj[j], o, 64);
-        const float d = (s2 - sj[j]) / n;
-        mj[j] = mj[j] + m2 + d * d * (0.5f * n);
-        sj[j] += s2;
-      }
-      n *= 2.f;
-    }
-    if (lq == 0)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red2[wm * BN + col_of(j)] = make_float2(sj[j], mj[j]);
-    __syncthreads();
-    if (wm == 0 && lq == 0) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c = col_of(j);
-        float2 t = red2[c];
-        float nt = (float)WM;
-#pragma unroll
-        for (int w = 1; w < WMW; ++w) {
-          const float2 u = red2[w * BN + c];
-          const float d = u.x / (float)WM - t.x / nt;
-          t.y = t.y + u.y + d * d * (nt * (float)WM / (nt + (float)WM));
-          t.x += u.x;
-          nt += (float)WM;
-        }
-        *(float2*)(a.stats + 2 * ((size_t)pt * a.Co + n0 + c)) = t;
-      }
-    }
-    __syncthreads();
   }
-  float* stage = (float*)smem;
-  E* Y = (E*)a.y;
-  const E* R1 = (const E*)a.r;
-  const E* R2 = (const E*)a.r2;
-  const int s_rl = tid >> 3, s_cc = tid & 7;
-#pragma unroll
-  for (int pass = 0; pass < BN / EPI_COLS; ++pass) {
-    const int cbase = pass * EPI_COLS;
-    if (wn * WN + WN > cbase && wn * WN < cbase + EPI_COLS) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int col = col_of(j);
-        if (col >= cbase && col < cbase + EPI_COLS) {
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) stage[row_of(i, k) * EPI_LD + (col - cbase)] = acc[i][j][k];
-        }
-      }
-    }
-    __syncthreads();
-    const int n = n0 + cbase + s_cc * 8;
-    {
-#pragma unroll
-      for (int rr = 0; rr < BM / 64; ++rr) {
-        const int row = s_rl + 64 * rr;
-        const int ty = row / PT_W, tx = row - ty * PT_W;
-        const long m = ((long)nimg * a.Ho + ty0 + ty) * a.Wo + tx0 + tx;
-        const float* sp = stage + row * EPI_LD + s_cc * 8;
-        const float4 v0 = *(const float4*)sp, v1 = *(const float4*)(sp + 4);
-        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        if (R1) {
-          float u[8];
-          Vec8<E>::load(R1 + (size_t)m * a.ldr + n, u);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += u[e];
-        }
-        if (R2) {
-          float u[8];
-          Vec8<E>::load(R2 + (size_t)m * a.ldr2 + n, u);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += u[e];
-        }
-        store8_nt(Y + (size_t)m * a.ldy + n, v);
-      }
-    }
-    __syncthreads();
-  }
+  __builtin_amdgcn_s_barrier();   // every wave's patch / weight reads done: LDS -> epilogue
+  patch_epilogue<E, BN, WMW, WNW>(a, acc, smem, pt, 0, nimg, ty0, tx0);
 }
 
 template <typename E, int BN, int WMW, int WNW, int NPB, int NST, int OCC>
@@ -709,6 +811,30 @@ hipError_t patch_launch(const ConvArgs& a, hipStream_t s) {
   }
   const int nwg = a.N * (a.Ho / PT_H) * (a.Wo / PT_W) * (a.Co / BN);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(V2_THREADS), LDS, s, a);
+  return hipGetLastError();
+}
+
+// the stem's patch kernel: the s2d tap mode with 64 output channels on whole 8 x 32 tiles
+bool conv_nt_patch_s2d_ok(const ConvArgs& a) {
+  static const bool on = [] { const char* e = getenv("SEG_PATCH"); return !(e && e[0] == '0'); }();
+  return on && a.tap8 == 2 && a.C == 16 && a.ldx == 16 && a.Co == 64 && a.KH == 4 && a.KW == 4 &&
+         a.sf == 1 && a.pad_h == 0 && a.pad_w == 0 && a.dil == 1 && a.ldw >= 256 && a.ldw % 8 == 0 &&
+         a.H == a.Ho + 3 && a.W == a.Wo + 3 && a.Ho % PT_H == 0 && a.Wo % PT_W == 0 && a.ldy % 8 == 0 &&
+         !a.r && !a.r2;
+}
+
+template <typename E>
+hipError_t patch_s2d_launch(const ConvArgs& a, hipStream_t s) {
+  constexpr int LDS = 256 * (64 + 4) * 4;   // the epilogue staging (> 16 KB patch + 32 KB weights)
+  static_assert(PS_PIX * 32 + 4 * 8192 <= LDS, "LDS");
+  auto kern = conv_nt_patch_s2d_kernel<E>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(a.N * (a.Ho / PT_H) * (a.Wo / PT_W)), dim3(V2_THREADS), LDS, s, a);
   return hipGetLastError();
 }
 
@@ -747,7 +873,7 @@ static bool v2_small_tile(const ConvArgs& a) { return a.Co <= 64; }
 int conv_nt_v2_rows(const ConvArgs& a) {
   // the ping-pong kernel writes one partial per wave row (128 rows), the v2 kernels per tile
   if (a.Co > 128 && !a.r && !a.r2 && conv_nt_pp_ok(a)) return 128;
-  if (conv_nt_patch_ok(a)) return 256;
+  if (conv_nt_patch_ok(a) || conv_nt_patch_s2d_ok(a)) return 256;
   return v2_small_tile(a) ? 128 : 256;
 }
 
@@ -772,6 +898,7 @@ hipError_t v2_dispatch(int dtype, const ConvArgs& a, hipStream_t s) {
 template <typename E>
 hipError_t nt_v2_e(int dtype, const ConvArgs& a, hipStream_t s) {
   if (a.tap8) {
+    if (conv_nt_patch_s2d_ok(a)) return patch_s2d_launch<E>(a, s);
     if (v2_small_tile(a)) return v2_launch<E, 64, 8, 1, 3, 1, 2, 16, 128>(a, s);
     return v2_launch<E, 64, 8, 1, 3, 1, 2>(a, s);
   }
