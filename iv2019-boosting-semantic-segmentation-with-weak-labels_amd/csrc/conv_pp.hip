@@ -5,19 +5,21 @@
 //
 //  * 256 x 256 tile, 8 waves as 2 (M) x 4 (N), each wave owns 128 rows x 64 columns split in
 //    four 64 x 32 quadrants;
-//  * every 64-deep K-tile is four PHASES, one per quadrant, in the order (qm,qn) = (0,0),
-//    (0,1), (1,1), (1,0); a phase is a LOAD segment (the ds_read_b128 fragments the quadrant
-//    needs that are not already in registers, plus one half-tile of LDS-DMA for the next
-//    K-tile) and an MFMA segment (16 x v_mfma_f32_16x16x32_bf16), separated by s_barrier;
+//  * every 64-deep K-tile is two PHASES of two quadrants each, (qm,qn) = (0,0), (0,1) then
+//    (1,1), (1,0); a phase is a LOAD segment (the ds_read_b128 fragments the quadrants need
+//    that are not already in registers, plus LDS-DMA of the next K-tile's halves: A0, B0, B1
+//    in phase 0, A1 in phase 1) and an MFMA segment (32 x v_mfma_f32_16x16x32_bf16),
+//    separated by s_barrier (round 2: four one-quadrant phases had twice the barriers; two
+//    phases run the block4 3x3 forward / data gradient 3-7 % faster, the step +1 %);
 //  * the two wave rows are staggered by one barrier (wave row 1 starts with an extra
 //    s_barrier), so on every SIMD one wave is in its MFMA segment while the other issues its
 //    LDS reads and DMA: the matrix pipe does not idle across barriers;
 //  * LDS holds two K-tile buffers, each four 16 KB half-tiles (A rows 0-127 / 128-255, B rows
-//    0-127 / 128-255). Phase i of K-tile k refills half ORDER[i] = A0, B0, B1, A1 of K-tile
-//    k+1 in the other buffer; every half is restaged >= 2 segments after its last ds_read
-//    (WAR) and waited for with a counted vmcnt before the barrier that precedes its first
-//    read (RAW): vmcnt(4) after phases 0, 1 and 3 (two later half-tiles = 4 DMAs per lane
-//    stay in flight), none after phase 2;
+//    0-127 / 128-255). K-tile k+1 goes into the other buffer, whose halves were last read in
+//    K-tile k-1 (by the lagging wave row one segment before the refill: WAR), and each half is
+//    waited for with a counted vmcnt before the barrier that precedes its first read (RAW):
+//    vmcnt(6) before phase 1 (A0, B0, B1 of k+1 in flight), vmcnt(2) before the next phase 0
+//    (A1 of k+1 in flight);
 //  * operands are fetched with buffer_load ... lds through buffer resources: a 32-bit byte
 //    offset per lane, padding taps and rows past the tensor given an out-of-range offset so
 //    the buffer unit writes zeros (4 VALU per A DMA, 1 per B DMA: the load segment is short);
@@ -275,50 +277,49 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   // A0, B0 of K-tile 0 landed (B1, A1 in flight; a previous tile's epilogue stores, issued
   // after them, count too and are waited for here)
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // A0, B0, B1 landed (A1 in flight)
   pp_barrier();
   if (wm == 1) pp_barrier();   // stagger: wave row 1 runs one segment behind
 
-  // wait after a phase for the halves the next phase reads first (see header)
-  auto wait_next = [&](bool more) {
-    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
-  for (int kb = 0; kb < nk; ++kb) {
-    const char* buf = smem + (kb & 1) * BUF;
-    const bool more = kb + 1 < nk;
-    const KT tn = ktile_next();   // K-tile kb + 1
-    // phase 0: quadrant (0,0), needs A0 + B0; refill A0 of kb+1
-    read_a(buf, 0);
-    read_b(buf, 0);
-    if (more) issue_half(kb + 1, tn, 0);
-    if (wm == 1) wait_next(more);
-    pp_barrier();
-    mfma_q(0, 0);
-    if (wm == 0) wait_next(more);
-    pp_barrier();
-    // phase 1: quadrant (0,1), needs B1; refill B0
-    read_b(buf, 1);
-    if (more) issue_half(kb + 1, tn, 2);
-    if (wm == 1) wait_next(more);
-    pp_barrier();
-    mfma_q(0, 1);
-    if (wm == 0) wait_next(more);
-    pp_barrier();
-    // phase 2: quadrant (1,1), needs A1; refill B1
-    read_a(buf, 1);
-    if (more) issue_half(kb + 1, tn, 3);
-    pp_barrier();
-    mfma_q(1, 1);
-    pp_barrier();
-    // phase 3: quadrant (1,0), B0 still in registers from phase 0; refill A1
-    if (more) issue_half(kb + 1, tn, 1);
-    if (more && wm == 1) wait_next(true);
-    pp_barrier();
-    mfma_q(1, 0);
-    if (more && wm == 0) wait_next(true);
-    pp_barrier();
+  {
+    // two phases per K-tile (half the barriers): phase 0 = quadrants (0,0), (0,1) from A0, B0,
+    // B1, refilling A0, B0, B1 of kb+1 (all read in phase 0 of kb-1 by both wave rows); phase 1
+    // = (1,1), (1,0) from A1, refilling A1 of kb+1. Waits: before phase 1, A1(kb) with the 6
+    // DMAs of phase 0 still in flight; before phase 0 of kb+1, its A0, B0, B1 with A1(kb+1) in
+    // flight
+    for (int kb = 0; kb < nk; ++kb) {
+      const char* buf = smem + (kb & 1) * BUF;
+      const bool more = kb + 1 < nk;
+      const KT tn = ktile_next();
+      read_a(buf, 0);
+      read_b(buf, 0);
+      read_b(buf, 1);
+      if (more) {
+        issue_half(kb + 1, tn, 0);
+        issue_half(kb + 1, tn, 2);
+        issue_half(kb + 1, tn, 3);
+      }
+      if (wm == 1) {
+        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pp_barrier();
+      mfma_q(0, 0);
+      mfma_q(0, 1);
+      if (wm == 0) {
+        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pp_barrier();
+      read_a(buf, 1);
+      if (more) issue_half(kb + 1, tn, 1);
+      if (more && wm == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      pp_barrier();
+      mfma_q(1, 1);
+      mfma_q(1, 0);
+      if (more && wm == 0) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      pp_barrier();
+    }
   }
   if (wm == 0) pp_barrier();   // realign the two wave rows: every LDS read of the tile is done
   PP_TS(dbg_it, 1);
@@ -596,9 +597,9 @@ hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s) {
 // ======================================================================================
 // 16-bit weight gradient, ping-pong schedule: C[co][tap*Ci+ci] = sum_p dy[p][co] * x[src(p,tap)][ci]
 //
-// The NT kernel's main loop transposed to the TN problem of conv_wgrad_v2_kernel: 256 (co) x
-// 256 (tap,ci) tile, 8 waves as 2 x 4 with 128 x 64 wave tiles in four 64 x 32 quadrants; a
-// K-tile is 64 pixels; each half-tile is 64 pixel rows x 256 B (128 co of dy, or 128 columns
+// The NT kernel's main loop (two phases of two quadrants per K-tile) transposed to the TN
+// problem of conv_wgrad_v2_kernel: 256 (co) x 256 (tap,ci) tile, 8 waves as 2 x 4 with 128 x 64
+// wave tiles in four 64 x 32 quadrants; a K-tile is 64 pixels; each half-tile is 64 pixel rows x 256 B (128 co of dy, or 128 columns
 // of the gathered x) read by ds_read_b64_tr_b16 through the XOR swizzle of the v2 kernel.
 // Operands come through buffer resources: dy rows are one add per DMA, x rows are decoded once
 // per K-tile and lane (pixel -> n, ho, wo by row carries) and shared by both x halves.
@@ -795,52 +796,53 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
         for (int j = 0; j < 2; ++j)
           acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfq[qn][j][s], acc[qm][qn][i][j]);
   };
-  auto wait_next = [&](bool more) {
-    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
   if (nk > 0) {
     decode_next();
     issue_half(0, 0);
     issue_half(0, 2);
     issue_half(0, 3);
     issue_half(0, 1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // halves 0, 2, 3 landed (1 in flight)
     pp_barrier();
     if (wm == 1) pp_barrier();
     // static priority for the second-dispatched wave row (waves 4-7, the arbitration loser);
     // per-segment priority flips measured 2-5 % slower on the wgrad 1x1 layers
     if (wm == 1) __builtin_amdgcn_s_setprio(1);
-    for (int kb = 0; kb < nk; ++kb) {
-      const bool more = kb + 1 < nk;
-      if (more) decode_next();   // K-tile kb + 1
-      read_a(kb, 0);
-      read_b(kb, 0);
-      if (more) issue_half(kb + 1, 0);
-      if (wm == 1) wait_next(more);
-      pp_barrier();
-      mfma_q(0, 0);
-      if (wm == 0) wait_next(more);
-      pp_barrier();
-      read_b(kb, 1);
-      if (more) issue_half(kb + 1, 2);
-      if (wm == 1) wait_next(more);
-      pp_barrier();
-      mfma_q(0, 1);
-      if (wm == 0) wait_next(more);
-      pp_barrier();
-      read_a(kb, 1);
-      if (more) issue_half(kb + 1, 3);
-      pp_barrier();
-      mfma_q(1, 1);
-      pp_barrier();
-      if (more) issue_half(kb + 1, 1);   // B0 is still in registers from phase 0
-      if (more && wm == 1) wait_next(true);
-      pp_barrier();
-      mfma_q(1, 0);
-      if (more && wm == 0) wait_next(true);
-      pp_barrier();
+    {
+      // two phases per K-tile as the NT kernel: (0,0), (0,1) from dy co 0-127 and both x
+      // halves, refilling those three of kb+1; then (1,1), (1,0) from dy co 128-255
+      for (int kb = 0; kb < nk; ++kb) {
+        const bool more = kb + 1 < nk;
+        if (more) decode_next();
+        read_a(kb, 0);
+        read_b(kb, 0);
+        read_b(kb, 1);
+        if (more) {
+          issue_half(kb + 1, 0);
+          issue_half(kb + 1, 2);
+          issue_half(kb + 1, 3);
+        }
+        if (wm == 1) {
+          if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        pp_barrier();
+        mfma_q(0, 0);
+        mfma_q(0, 1);
+        if (wm == 0) {
+          if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        pp_barrier();
+        read_a(kb, 1);
+        if (more) issue_half(kb + 1, 1);
+        if (more && wm == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        pp_barrier();
+        mfma_q(1, 1);
+        mfma_q(1, 0);
+        if (more && wm == 0) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        pp_barrier();
+      }
     }
     if (wm == 0) pp_barrier();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
