@@ -28,7 +28,7 @@ def main():
             w.writerows(table)
     for r in table[:25]:
         print(f"{r[4]:6.2f}%  {r[1]:6d}  avg {r[3] / 1e3:9.3f} us  {r[0][:110]}")
-    cls = {"conv_nt (fwd+dgrad)": ("conv_nt_kernel", "conv_nt_v2_kernel", "conv_nt_pp_kernel", "conv_nt_patch_kernel"),
+    cls = {"conv_nt (fwd+dgrad)": ("conv_nt_kernel", "conv_nt_v2_kernel", "conv_nt_pp_kernel", "conv_nt_patch_kernel", "conv_nt_patch_s2d_kernel"),
            "conv_wgrad": ("conv_wgrad_kernel", "conv_wgrad_v2_kernel", "conv_wgrad_pp_kernel")}
     for k, pats in cls.items():
         sel = [r for r in rows if any(f"::{p}<" in r[0] for p in pats)]
