@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--no-defer-stem", action="store_true",
+                    help="A/B: join every weight gradient before the update (the N > 1 order)")
     args = ap.parse_args()
 
     import numpy as np
@@ -139,6 +141,11 @@ def main():
     ctx = SegContext(depth=depth, pyramid=args.pyramid, height=H, width=W, nb_pp=nb_pp, nb_pb=nb_pb,
                      nb_pi=nb_pi, dtype=args.dtype, device=local, ema=ema_on)
     ctx.load_params(init_params(ctx.param_info, seed=0))
+    if world == 1 and args.dtype != "fp16" and not args.no_defer_stem:
+        # single process: the update of every parameter but the stem's runs beside the stem's
+        # weight gradient, the step's last kernel (define_estimator_hierarchical.train_op does
+        # the same); N > 1 updates after the all-reduce, fp16 after the overflow check
+        ctx.set_defer_stem(True)
     data = batch(1000 + rank, nb_pp, nb_pb, nb_pi, H, W)
     img = torch.as_tensor(data["images"]).to(dev)
     px = torch.as_tensor(data["px"]).to(dev) if nb_pp else None

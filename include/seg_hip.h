@@ -108,6 +108,13 @@ int seg_apply_update(seg_ctx* ctx, float lr, float momentum, float ema_decay_eff
 /* tf.train.MomentumOptimizer(use_nesterov=on) for later updates (define_optimizer.py:17-20):
  * var -= lr * (g + momentum * accum) instead of var -= lr * accum; off by default */
 int seg_set_nesterov(seg_ctx* ctx, int on);
+/* Overlap the update with the backward's last kernel (single-process training loops: nothing
+ * may read the gradients between seg_backward and seg_apply_update). With on, seg_backward
+ * returns with the stream joined to every weight gradient except the stem's, which is still
+ * running on the weight-gradient stream; seg_apply_update updates every other parameter beside
+ * it and joins before the stem's weights. Every other call that takes a stream joins first.
+ * No reference counterpart (scheduling only; results are unchanged). Off by default. */
+int seg_set_defer_stem(seg_ctx* ctx, int on);
 
 /* outputs ------------------------------------------------------------------------------
  * losses: device float[10] = {segmentation, l1, l2_vehicle, l2_human, n1, n2v, n2h,

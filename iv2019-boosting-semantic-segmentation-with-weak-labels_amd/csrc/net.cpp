@@ -192,6 +192,13 @@ struct seg_ctx {
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> ev_dy;   // per conv: dy written on the compute stream
   hipEvent_t ev_join = nullptr;
+  // seg_set_defer_stem: the backward's compute stream joins the weight-gradient stream before the
+  // stem's weight gradient (ev_prestem) instead of after it; seg_apply_update updates every other
+  // parameter beside that last kernel and joins (ev_join) before the stem's weights
+  hipEvent_t ev_prestem = nullptr;
+  bool defer_stem = false;
+  bool prestem_rec = false;
+  bool stem_pending = false;
   float* dzscale = nullptr;       // [ldl]
   float* reg_part = nullptr;
   float* reg_out = nullptr;
@@ -726,6 +733,10 @@ int conv_wgrad(Step& S, int li, const Act& x) {
   seg_ctx* c = S.c;
   Step W = S;
   if (c->side_active) {   // the layer's dy (and the wgrad input x) are ready on the compute stream
+    if (li == c->stem && c->defer_stem) {   // every other weight gradient is queued before it
+      HIPCALL(c, hipEventRecord(c->ev_prestem, c->side));
+      c->prestem_rec = true;
+    }
     HIPCALL(c, hipEventRecord(c->ev_dy[li], S.s));
     HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_dy[li], 0));
     W.s = c->side;
@@ -962,6 +973,7 @@ int build(seg_ctx* c) {
       c->ev_dy.resize(c->convs.size());
       for (auto& ev : c->ev_dy) HIPCALL(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       HIPCALL(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+      HIPCALL(c, hipEventCreateWithFlags(&c->ev_prestem, hipEventDisableTiming));
     }
   }
   for (auto& L : c->convs) {
@@ -1103,7 +1115,7 @@ int build(seg_ctx* c) {
   if (int r = dalloc(c, &c->loss_part, (size_t)c->loss_blocks * 8)) return r;
   if (int r = dalloc(c, &c->loss_out, 16)) return r;
   if (int r = dalloc(c, &c->dzscale, c->ldl)) return r;
-  if (int r = dalloc(c, &c->reg_part, sgdm_blocks(c->n_decay))) return r;
+  if (int r = dalloc(c, &c->reg_part, sgdm_blocks(c->n_decay) + 2)) return r;   // + the split update's
   if (int r = dalloc(c, &c->reg_out, 4)) return r;
 
   // ---- compute weight copies and workspace ----
@@ -1288,6 +1300,7 @@ int backward(Step& S) {
   c->bk_next = 0;
   // a profiled backward runs on one stream so the HIP-event kernel timings are kernel-alone
   c->side_active = c->side_on && !c->prof.on;
+  c->prestem_rec = false;
   if (c->side_active) {   // the side stream must not run ahead of the previous use of its buffers
     HIPCALL(c, hipEventRecord(c->ev_join, S.s));
     HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
@@ -1296,7 +1309,12 @@ int backward(Step& S) {
   if (int r = bucket_progress(c, c->side_active ? c->side : S.s, true)) return r;
   if (c->side_active) {   // join: the update (and the next forward) follow every weight gradient
     HIPCALL(c, hipEventRecord(c->ev_join, c->side));
-    HIPCALL(c, hipStreamWaitEvent(S.s, c->ev_join, 0));
+    if (c->prestem_rec) {   // deferred: only the gradients before the stem's (see seg_apply_update)
+      HIPCALL(c, hipStreamWaitEvent(S.s, c->ev_prestem, 0));
+      c->stem_pending = true;
+    } else {
+      HIPCALL(c, hipStreamWaitEvent(S.s, c->ev_join, 0));
+    }
   }
   // BN-parameter + statistics tail bucket: written on the compute stream
   HIPCALL(c, hipEventRecord(c->bk_ev.back(), S.s));
@@ -1390,6 +1408,15 @@ int refresh_stem_pad(seg_ctx* c, hipStream_t s) {
   if (!c->stem_s2d) return 0;
   const ConvL& st = c->convs[c->stem];
   HIPCALL(c, launch_stem_s2d_weights((const bf16_t*)st.w_lp, c->stem_wpad, st.co, s));
+  return 0;
+}
+
+// a deferred stem weight gradient (seg_set_defer_stem) must be complete before anything else
+// on stream s reads or rewrites the step's buffers
+int join_stem(seg_ctx* c, hipStream_t s) {
+  if (!c->stem_pending) return 0;
+  c->stem_pending = false;
+  HIPCALL(c, hipStreamWaitEvent(s, c->ev_join, 0));
   return 0;
 }
 
@@ -1512,6 +1539,7 @@ int seg_param_shape(seg_ctx* c, int64_t i, int64_t* dims) {
 
 int seg_params_updated(seg_ctx* c, void* stream) {
   NEED_BOUND(c);
+  if (int r = join_stem(c, (hipStream_t)stream)) return r;
   return refresh_compute_weights(c, (hipStream_t)stream);
 }
 
@@ -1519,12 +1547,14 @@ int seg_forward(seg_ctx* c, const float* images, void* stream) {
   NEED_BOUND(c);
   if (!images) return set_err(&c->err, -EINVAL, "images required");
   Step S{c, (hipStream_t)stream, c->dt};
+  if (int r = join_stem(c, S.s)) return r;
   return forward(S, images);
 }
 
 int seg_loss(seg_ctx* c, const int32_t* px, const float* bbox, const float* tag, int32_t* decisions,
              void* stream) {
   NEED_BOUND(c);
+  if (int r = join_stem(c, (hipStream_t)stream)) return r;
   const seg_cfg& g = c->cfg;
   if ((g.nb_pp && !px) || (g.nb_pb && !bbox) || (g.nb_pi && !tag))
     return set_err(&c->err, -EINVAL, "missing labels for a non-empty sub-batch");
@@ -1564,6 +1594,7 @@ int seg_set_bn_inference(seg_ctx* c, int on) {
 int seg_predict(seg_ctx* c, const int32_t* cid_map, int n_map, int replace_voids, int out_h,
                 int out_w, int32_t* decisions_out, void* stream) {
   NEED_BOUND(c);
+  if (int r = join_stem(c, (hipStream_t)stream)) return r;
   const seg_cfg& g = c->cfg;
   if (!cid_map || !decisions_out) return set_err(&c->err, -EINVAL, "null cid_map / decisions_out");
   if (n_map != c->tables.n_pp)
@@ -1587,6 +1618,7 @@ int seg_predict(seg_ctx* c, const int32_t* cid_map, int n_map, int replace_voids
 int seg_full_predictions(seg_ctx* c, float* logits_out, float* probs_out,
                          int32_t* head_decisions_out, int32_t* decisions_out, void* stream) {
   NEED_BOUND(c);
+  if (int r = join_stem(c, (hipStream_t)stream)) return r;
   FullPredArgs a{};
   a.logits = c->head_in; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
   a.ldl = c->ldl; a.H = c->cfg.height; a.W = c->cfg.width;
@@ -1601,6 +1633,7 @@ int seg_full_predictions(seg_ctx* c, float* logits_out, float* probs_out,
 int seg_backward(seg_ctx* c, void* stream) {
   NEED_BOUND(c);
   Step S{c, (hipStream_t)stream, c->dt};
+  if (int r = join_stem(c, S.s)) return r;
   return backward(S);
 }
 
@@ -1608,6 +1641,15 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
                      void* stream) {
   NEED_BOUND(c);
   hipStream_t s = (hipStream_t)stream;
+  const ConvL& stl = c->convs[c->stem];
+  const long st_lo = stl.w_off, st_hi = stl.w_off + (long)stl.co * stl.k * stl.k * stl.ci;
+  // deferred stem (seg_set_defer_stem): every parameter but the stem's conv weights is updated
+  // while the stem's weight gradient still runs on the weight-gradient stream; not with loss
+  // scaling (one overflow check covers all gradients) or a gradient scale (the all-reduce path)
+  const bool split = c->stem_pending && !c->skip_flag && grad_scale == 1.f && !stl.wt_lp &&
+                     st_hi <= c->n_decay;
+  if (!split)
+    if (int r = join_stem(c, s)) return r;
   if (c->skip_flag) {   // loss-scaled (fp16) step: unscale, and skip it if anything overflowed
     HIPCALL(c, hipMemsetAsync(c->skip_flag, 0, sizeof(int), s));
     HIPCALL(c, launch_nonfinite(c->grads, c->n_train, c->skip_flag, s));
@@ -1623,8 +1665,29 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
   a.skip = c->skip_flag;
   a.n = c->n_decay; a.lr = lr; a.momentum = momentum; a.wd = c->cfg.weight_decay;
   a.ema_decay = ema_decay_eff; a.reg_part = c->reg_part; a.nesterov = c->nesterov;
-  HIPCALL(c, launch_sgdm(a, s));
-  HIPCALL(c, launch_sum_partials(c->reg_part, sgdm_blocks(c->n_decay), c->reg_out, s));
+  int nparts = sgdm_blocks(c->n_decay);
+  SgdmArgs st_a = a;   // the stem's range (split): [st_lo, st_hi), partials after the others'
+  if (split) {
+    // [0, st_lo) and [st_hi, n_decay) now, partials packed in that order, then the stem's
+    SgdmArgs r0 = a, r1 = a;
+    r0.n = st_lo;
+    r1.w = a.w + st_hi; r1.g = a.g + st_hi; r1.v = a.v + st_hi;
+    r1.ema = a.ema ? a.ema + st_hi : nullptr;
+    r1.w_lp = a.w_lp ? (char*)a.w_lp + st_hi * c->esz : nullptr;
+    r1.n = c->n_decay - st_hi;
+    r1.reg_part = a.reg_part + sgdm_blocks(r0.n);
+    HIPCALL(c, launch_sgdm(r0, s));
+    HIPCALL(c, launch_sgdm(r1, s));
+    st_a.w = a.w + st_lo; st_a.g = a.g + st_lo; st_a.v = a.v + st_lo;
+    st_a.ema = a.ema ? a.ema + st_lo : nullptr;
+    st_a.w_lp = a.w_lp ? (char*)a.w_lp + st_lo * c->esz : nullptr;
+    st_a.n = st_hi - st_lo;
+    st_a.reg_part = r1.reg_part + sgdm_blocks(r1.n);
+    nparts = sgdm_blocks(r0.n) + sgdm_blocks(r1.n) + sgdm_blocks(st_a.n);
+  } else {
+    HIPCALL(c, launch_sgdm(a, s));
+    HIPCALL(c, launch_sum_partials(c->reg_part, nparts, c->reg_out, s));
+  }
   if (c->cfg.train_bn) {
     SgdmArgs b = a;
     b.w = c->params + c->n_decay; b.g = c->grads + c->n_decay; b.v = c->mom + c->n_decay;
@@ -1644,7 +1707,18 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
     HIPCALL(c, launch_moving_update(c->moving, c->moving + half, c->grads + c->n_train,
                                     c->grads + c->n_train + half, (int)half, c->cfg.bn_decay, s));
   if (c->n_flip) HIPCALL(c, launch_weight_flip_batched(c->dt, c->flip_jobs, c->n_flip, c->flip_total, s));
+  if (split) {   // the stem's weight gradient is done: its update, then the regulariser sum
+    if (int r = join_stem(c, s)) return r;
+    HIPCALL(c, launch_sgdm(st_a, s));
+    HIPCALL(c, launch_sum_partials(c->reg_part, nparts, c->reg_out, s));
+  }
   return refresh_stem_pad(c, s);
+}
+
+int seg_set_defer_stem(seg_ctx* c, int on) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  c->defer_stem = on != 0;
+  return 0;
 }
 
 int seg_outputs(seg_ctx* c, const float** losses, const float** reg, const float** logits,

@@ -10,6 +10,34 @@ __global__ void sgdm_kernel(SgdmArgs a) {
   const long base = (long)blockIdx.x * SG_PER_BLOCK;
   const bool skip = a.skip && *a.skip;   // dynamic loss scaling: overflowed step
   float reg = 0.f;
+  if (base + SG_PER_BLOCK <= a.n && !skip) {
+    // whole block: branch-free, so every element's loads are issued ahead of the arithmetic
+    // (the bounds check in the general loop serialised one memory latency per element)
+    float w_old[16], g[16], v[16], e[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const long i = base + (long)k * SG_THREADS + threadIdx.x;
+      w_old[k] = a.w[i];
+      g[k] = a.g[i];
+      v[k] = a.v[i];
+      if (a.ema) e[k] = a.ema[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const long i = base + (long)k * SG_THREADS + threadIdx.x;
+      reg += w_old[k] * w_old[k];
+      const float gt = g[k] + a.wd * w_old[k];
+      const float vn = v[k] * a.momentum + gt;
+      a.v[i] = vn;
+      const float w_new = a.nesterov ? w_old[k] - a.lr * (gt + a.momentum * vn) : w_old[k] - a.lr * vn;
+      a.w[i] = w_new;
+      if (a.ema) a.ema[i] = e[k] - (1.f - a.ema_decay) * (e[k] - w_old[k]);
+      if (a.w_lp) {
+        if (a.lp_f16) ((f16_t*)a.w_lp)[i] = (f16_t)w_new;
+        else ((bf16_t*)a.w_lp)[i] = f2bf(w_new);
+      }
+    }
+  } else
   for (int k = 0; k < 16; ++k) {
     const long i = base + (long)k * SG_THREADS + threadIdx.x;
     if (i >= a.n) break;

@@ -32,18 +32,22 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W,
     uint32_t am[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { mx[e] = -INFINITY; am[e] = 255; }
-    for (int dh = 0; dh < 3; ++dh) {
-      int hi = ho * 2 - ph + dh;
-      if (hi < 0 || hi >= H) continue;
-      for (int dw = 0; dw < 3; ++dw) {
-        int wi = wo * 2 - pw + dw;
-        if (wi < 0 || wi >= W) continue;
-        float v[8];
-        Vec8<T>::load(x + ((size_t)((long)n * H + hi) * W + wi) * ldx + cg * 8, v);
+    // the 9 window rows are loaded before any compare (one memory latency per element, not 9);
+    // padding taps read a valid in-range row and are skipped
+    float v[9][8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (v[e] > mx[e]) { mx[e] = v[e]; am[e] = dh * 3 + dw; }  // first max wins
-      }
+    for (int t9 = 0; t9 < 9; ++t9) {
+      const int hi = ho * 2 - ph + t9 / 3, wi = wo * 2 - pw + t9 % 3;
+      const int hc = hi < 0 ? 0 : (hi >= H ? H - 1 : hi), wc = wi < 0 ? 0 : (wi >= W ? W - 1 : wi);
+      Vec8<T>::load(x + ((size_t)((long)n * H + hc) * W + wc) * ldx + cg * 8, v[t9]);
+    }
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+      const int hi = ho * 2 - ph + t9 / 3, wi = wo * 2 - pw + t9 % 3;
+      if (hi < 0 || hi >= H || wi < 0 || wi >= W) continue;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (v[t9][e] > mx[e]) { mx[e] = v[t9][e]; am[e] = t9; }  // first max wins (row-major scan)
     }
     Vec8<T>::store(y + p * ldy + cg * 8, mx);
     uint2 packed;
@@ -73,24 +77,38 @@ __global__ __launch_bounds__(256) void maxpool_bwd_row_kernel(
   const int ho_hi = (hi + ph) >> 1;
   const int wo_lo = wi + pw - 2 < 0 ? 0 : (wi + pw - 1) >> 1;
   const int wo_hi = (wi + pw) >> 1;
-  for (int ho = ho_lo; ho <= ho_hi && ho < Ho; ++ho) {
-    for (int wo = wo_lo; wo <= wo_hi && wo < Wo; ++wo) {
-      const size_t q = (size_t)((long)n * Ho + ho) * Wo + wo;
-      const uint2 a = *(const uint2*)(arg + q * C + cg * 8);
-      const uint32_t me = (uint32_t)((hi - (ho * 2 - ph)) * 3 + (wi - (wo * 2 - pw)));
-      uint32_t b[8] = {a.x & 255, (a.x >> 8) & 255, (a.x >> 16) & 255, a.x >> 24,
-                       a.y & 255, (a.y >> 8) & 255, (a.y >> 16) & 255, a.y >> 24};
-      bool any = false;
+  // the <= 2 x 2 covering windows: every argmax word and every gradient row is loaded before
+  // any is used (one memory latency per thread instead of one or two per window; the
+  // gradient rows of windows that did not pick this pixel are L2 reads, not HBM)
+  uint2 am[2][2];
+  float g[2][2][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) any |= b[e] == me;
-      if (!any) continue;
-      float g[8];
-      Vec8<T>::load(dy + q * lddy + cg * 8, g);
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ho = ho_lo + i, wo = wo_lo + j;
+      const bool ok = ho <= ho_hi && ho < Ho && wo <= wo_hi && wo < Wo;
+      const size_t q = (size_t)((long)n * Ho + (ok ? ho : 0)) * Wo + (ok ? wo : 0);
+      am[i][j] = ok ? *(const uint2*)(arg + q * C + cg * 8) : make_uint2(~0u, ~0u);
+      if (ok) Vec8<T>::load(dy + q * lddy + cg * 8, g[i][j]);
+      else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[i][j][e] = 0.f;
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      // window order and float order as the per-window loop: ho outer, wo inner
+      const uint32_t me = (uint32_t)((hi - ((ho_lo + i) * 2 - ph)) * 3 + (wi - ((wo_lo + j) * 2 - pw)));
+      const uint2 a = am[i][j];
+      const uint32_t b[8] = {a.x & 255, (a.x >> 8) & 255, (a.x >> 16) & 255, a.x >> 24,
+                             a.y & 255, (a.y >> 8) & 255, (a.y >> 16) & 255, a.y >> 24};
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        if (b[e] == me) acc[e] += g[e];
+        if (b[e] == me) acc[e] += g[i][j][e];
     }
-  }
   Vec8<T>::store(dx + ((size_t)((long)n * H + hi) * W + wi) * lddx + cg * 8, acc);
 }
 

@@ -104,6 +104,10 @@ def define_estimator(mode, features, labels, model_fn, config, params):
     optimizer = define_optimizer(global_step, params)
     if getattr(ctx, 'nesterov', False) != optimizer.use_nesterov:
         ctx.set_nesterov(optimizer.use_nesterov)
+    # one process: nothing reads the gradients between backward and update, so the update of
+    # every parameter but the stem's runs beside the stem's weight gradient (seg_set_defer_stem)
+    if world_size() <= 1 and getattr(ctx, 'dtype', None) != 'fp16' and hasattr(ctx, 'set_defer_stem'):
+        ctx.set_defer_stem(True)
 
     def train_op():
         ctx.backward()

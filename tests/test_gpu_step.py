@@ -208,6 +208,43 @@ def test_bf16_step_is_deterministic(cuda):
         assert np.array_equal(a["params"][k], b["params"][k]), k
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_defer_stem_update_matches(cuda, dtype):
+    """seg_set_defer_stem (the update of every parameter but the stem's beside the stem's weight
+    gradient, then the stem's): three steps with EMA give bitwise the same parameters, momentum
+    and EMA shadows as the joined update; the regulariser value (a sum in another order) 1e-6."""
+    from input_pipelines.synthetic import batch
+    from seg_hip import SegContext
+    cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=9).items()}
+    data = batch(21, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
+    img = torch.as_tensor(data["images"]).to(cuda)
+    px = torch.as_tensor(data["px"]).to(cuda)
+    bb = torch.as_tensor(data["bbox"]).to(cuda)
+    out = []
+    for defer in (False, True):
+        ctx = SegContext(pyramid=cfg.pyramid, height=cfg.height, width=cfg.width, nb_pp=1, nb_pb=1,
+                         dtype=dtype, ema=True)
+        ctx.load_params(params)
+        ctx.set_defer_stem(defer)
+        regs = []
+        for step in range(3):
+            ctx.forward(img)
+            ctx.loss(px, bb, None)
+            ctx.backward()
+            ctx.apply_update(0.01, 0.9, min(0.9, (1.0 + step) / (10.0 + step)))
+            torch.cuda.synchronize()
+            regs.append(float(ctx.outputs()[1].cpu().numpy()[0]))
+        out.append((ctx.named("params"), ctx.momentum.cpu().numpy().copy(),
+                    ctx.ema.cpu().numpy().copy(), regs))
+        ctx.close()
+    (p0, m0, e0, r0), (p1, m1, e1, r1) = out
+    for k in p0:
+        assert np.array_equal(p0[k], p1[k]), k
+    assert np.array_equal(m0, m1) and np.array_equal(e0, e1)
+    assert np.allclose(r0, r1, rtol=1e-6), (r0, r1)
+
+
 @pytest.mark.parametrize("nesterov", [False, True], ids=["momentum", "nesterov"])
 def test_two_step_fp32(cuda, nesterov):
     """Step 2 starts from the native step-1 state: its forward (losses, logits) matches the

@@ -41,3 +41,10 @@ for a, b in iv:
         cur_b = max(cur_b, b)
 tot += cur_b - cur_a
 print(f"GPU busy (any stream): {tot / 1e6:.2f} ms of {(t1 - t0) / 1e6:.2f}")
+
+# optional: the last N kernels of the step per stream (start offset, duration, name)
+if len(sys.argv) > 2:
+    n_tail = int(sys.argv[2])
+    print(f"last {n_tail} kernels of the step (offset ms from step start, duration us):")
+    for n, s, q, a, b in step[-n_tail:]:
+        print(f"  s{s}/q{q}  {(a - t0) / 1e6:8.3f}  {(b - a) / 1e3:8.1f}  {n[:90]}")
