@@ -129,6 +129,7 @@ struct seg_ctx {
   long flip_total = 0;
   bf16_t* stem_wpad = nullptr;
   Act z0, dz0, p0, dp0;
+  bool z0_stale = false;   // the fused stem BN + ReLU + max-pool did not store z0 (see forward)
   uint8_t* pool_arg = nullptr;    // max-pool first-max window index per output element
   int pool_ph = 0, pool_pw = 0;
   std::vector<Unit> units;
@@ -1232,10 +1233,28 @@ int forward(Step& S, const float* images) {
                               hipMemcpyDeviceToDevice, S.s));
   }
   if (int r = conv_forward(S, c->stem, c->img)) return r;
-  if (int r = bn_apply(S, c->stem, c->z0, 0)) return r;
-  HIPCALL(c, launch_maxpool_fwd(S.dt, c->z0.p, c->z0.N, c->z0.H, c->z0.W, 64, c->z0.ld, c->p0.p,
-                                c->p0.H, c->p0.W, c->p0.ld, c->pool_ph, c->pool_pw, c->pool_arg,
-                                S.s));
+  const ConvL& stl = c->convs[c->stem];
+  if (!c->gn && c->z0.mask && c->pool_ph == 0 && c->pool_pw == 0 && c->z0.H == 2 * c->p0.H &&
+      c->z0.W == 2 * c->p0.W) {
+    // stem BN + ReLU fused into the max-pool: y0 is read once, z0 (the max-pool input) is never
+    // written; its ReLU bits (the BN backward's gate) are
+    const double esz = c->esz;
+    const double gb = (c->z0.M() * 64.0 * (esz + 0.125) + c->p0.M() * 64.0 * (esz + 1.0)) * 1e-9;
+    int slot;
+    if (int r = prof_begin(c, S.s, 3, c->stem, gb, &slot)) return r;
+    HIPCALL(c, launch_bn_relu_maxpool_fwd(S.dt, stl.y.p, c->z0.N, c->z0.H, c->z0.W, stl.y.ld,
+                                          stl.st.mean, stl.st.scale, c->params + stl.b_off,
+                                          c->z0.mask, c->p0.p, c->p0.H, c->p0.W, c->p0.ld,
+                                          c->pool_ph, c->pool_pw, c->pool_arg, S.s));
+    if (int r = prof_end(c, S.s, slot)) return r;
+    c->z0_stale = true;
+  } else {
+    if (int r = bn_apply(S, c->stem, c->z0, 0)) return r;
+    HIPCALL(c, launch_maxpool_fwd(S.dt, c->z0.p, c->z0.N, c->z0.H, c->z0.W, 64, c->z0.ld, c->p0.p,
+                                  c->p0.H, c->p0.W, c->p0.ld, c->pool_ph, c->pool_pw, c->pool_arg,
+                                  S.s));
+    c->z0_stale = false;
+  }
   for (auto& u : c->units)
     if (int r = unit_forward(S, u)) return r;
   if (int r = conv_forward(S, c->dfd, c->units.back().out)) return r;
@@ -1856,7 +1875,15 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
   else if (n == "dzscale") { a.p = c->dzscale; a.N = a.H = a.W = 1; a.C = a.ld = c->ldl; dt = SEG_DTYPE_F32; }
   else if (n == "feat") a = c->feat;
   else if (n == "dfeat") a = c->dfeat;
-  else if (n == "z0") a = c->z0;   // stem BN + ReLU output (the max-pool input)
+  else if (n == "z0") {   // stem BN + ReLU output (the max-pool input)
+    if (c->z0_stale) {   // fused forward: materialise it (same kernel, this step's statistics)
+      Step S{c, nullptr, c->dt};
+      if (int r = bn_apply(S, c->stem, c->z0, 0)) return r;
+      HIPCALL(c, hipStreamSynchronize(nullptr));
+      c->z0_stale = false;
+    }
+    a = c->z0;
+  }
   else if (n.rfind("head", 0) == 0 && n.size() > 5) {
     int h = n[4] - '0';
     if (h < 0 || h > 2) return set_err(&c->err, -EINVAL, "bad head");

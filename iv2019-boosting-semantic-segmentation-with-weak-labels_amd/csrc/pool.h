@@ -26,6 +26,14 @@ struct GridSpec {
 hipError_t launch_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int ldx,
                               void* y, int Ho, int Wo, int ldy, int pad_h, int pad_w, void* arg,
                               hipStream_t s);
+// the stem's BN apply + ReLU fused into the 3x3/2 max-pool (C = 64, even H and W, no top / left
+// padding): z = relu((y - mean) * scale + beta) is rounded to the storage type per window tap
+// and pooled as the max-pool would pool the stored z; the ReLU bits of every input pixel are
+// written by the one window whose top-left 2 x 2 holds it; z itself is never stored
+hipError_t launch_bn_relu_maxpool_fwd(int dtype, const void* y, int N, int H, int W, int ldy,
+                                      const float* mean, const float* scale, const float* beta,
+                                      uint8_t* mask, void* p, int Ho, int Wo, int ldp, int pad_h,
+                                      int pad_w, uint8_t* arg, hipStream_t s);
 hipError_t launch_maxpool_bwd(int dtype, const void* arg, int N, int H, int W, int C,
                               const void* dy, int Ho, int Wo, int lddy, void* dx, int lddx,
                               int pad_h, int pad_w, hipStream_t s);

@@ -57,6 +57,61 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, int N, int H, int W,
   }
 }
 
+template <typename T>
+__global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(
+    const T* __restrict__ y, int N, int H, int W, int ldy, const float* __restrict__ mean,
+    const float* __restrict__ scale, const float* __restrict__ beta, uint8_t* __restrict__ mask,
+    T* __restrict__ p, int Ho, int Wo, int ldp, uint8_t* __restrict__ arg) {
+  constexpr int C = 64;
+  const unsigned total = (unsigned)N * Ho * Wo * 8;
+  const unsigned it = blockIdx.x * 256u + threadIdx.x;
+  if (it >= total) return;
+  const unsigned up = it >> 3;
+  const int cg = (int)(it & 7);
+  const unsigned ut = up / (unsigned)Wo;
+  const int wo = (int)(up - ut * (unsigned)Wo);
+  const unsigned un = ut / (unsigned)Ho;
+  const int ho = (int)(ut - un * (unsigned)Ho);
+  float mu[8], sc[8], be[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { mu[e] = mean[cg * 8 + e]; sc[e] = scale[cg * 8 + e]; be[e] = beta[cg * 8 + e]; }
+  // window taps (2ho + dh, 2wo + dw); taps past the bottom / right edge read a clamped row and
+  // are skipped (they are the 'SAME' padding)
+  float v[9][8];
+#pragma unroll
+  for (int t9 = 0; t9 < 9; ++t9) {
+    const int hi = ho * 2 + t9 / 3, wi = wo * 2 + t9 % 3;
+    const int hc = hi < H ? hi : H - 1, wc = wi < W ? wi : W - 1;
+    Vec8<T>::load(y + ((size_t)((long)un * H + hc) * W + wc) * ldy + cg * 8, v[t9]);
+  }
+  float mx[8];
+  uint32_t am[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { mx[e] = -INFINITY; am[e] = 255; }
+#pragma unroll
+  for (int t9 = 0; t9 < 9; ++t9) {
+    const int dh = t9 / 3, dw = t9 % 3;
+    const int hi = ho * 2 + dh, wi = wo * 2 + dw;
+    if (hi >= H || wi >= W) continue;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // the BN apply kernel's arithmetic and rounding: the value the max-pool would have read
+      const float o = fmaxf(__builtin_fmaf(v[t9][e] - mu[e], sc[e], be[e]), 0.f);
+      const float z = sizeof(T) == 2 ? TypeOps<T>::to_f(TypeOps<T>::from_f(o)) : o;
+      bits |= (uint32_t)(z > 0.f) << e;
+      if (z > mx[e]) { mx[e] = z; am[e] = t9; }   // first max wins (row-major scan)
+    }
+    if (dh < 2 && dw < 2)   // this window's top-left 2 x 2 owns the pixel's ReLU bits
+      mask[((size_t)((long)un * H + hi) * W + wi) * (C / 8) + cg] = (uint8_t)bits;
+  }
+  Vec8<T>::store(p + (size_t)up * ldp + cg * 8, mx);
+  uint2 packed;
+  packed.x = am[0] | (am[1] << 8) | (am[2] << 16) | (am[3] << 24);
+  packed.y = am[4] | (am[5] << 8) | (am[6] << 16) | (am[7] << 24);
+  *(uint2*)(arg + (size_t)up * C + cg * 8) = packed;
+}
+
 // gather form: each input pixel sums the gradients of the (<= 4) windows whose stored first
 // max (forward argmax byte) is this pixel — no atomics, no recomputation
 // C = 64 (the stem pool): blockIdx.y is one input row (n, hi) so the row decode is scalar;
@@ -411,6 +466,26 @@ hipError_t launch_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, dim3(256), 0, s, (const float*)x, N, H, W, C,
                        ldx, (float*)y, Ho, Wo, ldy, pad_h, pad_w, (uint8_t*)arg);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_relu_maxpool_fwd(int dtype, const void* y, int N, int H, int W, int ldy,
+                                      const float* mean, const float* scale, const float* beta,
+                                      uint8_t* mask, void* p, int Ho, int Wo, int ldp, int pad_h,
+                                      int pad_w, uint8_t* arg, hipStream_t s) {
+  if (pad_h || pad_w || H % 2 || W % 2 || Ho * 2 != H || Wo * 2 != W || ldy % 8 || ldp % 8)
+    return hipErrorInvalidValue;
+  if ((long)N * Ho * Wo * 8 >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit decode
+  const dim3 g((unsigned)ceil_div((long)N * Ho * Wo * 8, 256));
+  if (dtype == SEG_BF16)
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)y, N, H, W,
+                       ldy, mean, scale, beta, mask, (bf16_t*)p, Ho, Wo, ldp, arg);
+  else if (dtype == SEG_F16)
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel<f16_t>, g, dim3(256), 0, s, (const f16_t*)y, N, H, W,
+                       ldy, mean, scale, beta, mask, (f16_t*)p, Ho, Wo, ldp, arg);
+  else
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel<float>, g, dim3(256), 0, s, (const float*)y, N, H, W,
+                       ldy, mean, scale, beta, mask, (float*)p, Ho, Wo, ldp, arg);
   return hipGetLastError();
 }
 
