@@ -816,8 +816,7 @@ hipError_t patch_launch(const ConvArgs& a, hipStream_t s) {
 
 // the stem's patch kernel: the s2d tap mode with 64 output channels on whole 8 x 32 tiles
 bool conv_nt_patch_s2d_ok(const ConvArgs& a) {
-  static const bool on = [] { const char* e = getenv("SEG_PATCH"); return !(e && e[0] == '0'); }();
-  return on && a.tap8 == 2 && a.C == 16 && a.ldx == 16 && a.Co == 64 && a.KH == 4 && a.KW == 4 &&
+  return a.tap8 == 2 && a.C == 16 && a.ldx == 16 && a.Co == 64 && a.KH == 4 && a.KW == 4 &&
          a.sf == 1 && a.pad_h == 0 && a.pad_w == 0 && a.dil == 1 && a.ldw >= 256 && a.ldw % 8 == 0 &&
          a.H == a.Ho + 3 && a.W == a.Wo + 3 && a.Ho % PT_H == 0 && a.Wo % PT_W == 0 && a.ldy % 8 == 0 &&
          !a.r && !a.r2;
@@ -838,10 +837,10 @@ hipError_t patch_s2d_launch(const ConvArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// the patch kernel's shapes (see above); SEG_PATCH=0 turns it off (A/B)
+// the patch kernel's shapes (see above; measured against the v2 gather in
+// profiles/r02_ab_v19_patch_stem.txt)
 bool conv_nt_patch_ok(const ConvArgs& a) {
-  static const bool on = [] { const char* e = getenv("SEG_PATCH"); return !(e && e[0] == '0'); }();
-  return on && !a.tap8 && a.st == 1 && a.sf == 1 && a.dil == 1 && a.KH == 3 && a.KW == 3 &&
+  return !a.tap8 && a.st == 1 && a.sf == 1 && a.dil == 1 && a.KH == 3 && a.KW == 3 &&
          (a.C == 64 || a.C == 128) && (a.Co == 64 || a.Co == 128) && a.ldw == 9 * a.C &&
          a.H == a.Ho && a.W == a.Wo && a.Ho % PT_H == 0 && a.Wo % PT_W == 0 &&
          a.pad_h >= 0 && a.pad_h <= 2 && a.pad_w >= 0 && a.pad_w <= 2 &&
