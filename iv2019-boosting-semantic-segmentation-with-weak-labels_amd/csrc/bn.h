@@ -44,6 +44,13 @@ struct BnBwdArgs {
   const float* dzscale;            // optional per-channel factor applied to dz
   float* part;                     // reduce partials [rb][C][2]
   int rb;                          // number of row blocks
+  // dual (launch_bn_bwd_*_dual): a second BN layer gated by the same dz and bits, e.g. a
+  // projection unit's conv3 and shortcut BN; dz and the bits are read once for both
+  const void* y2; int ldy2;
+  const float* mean2; const float* invstd2; const float* scale2;
+  const float* sdy2; const float* sdyx2;
+  void* dy2; int lddy2;
+  float* part2;
 };
 
 // pack (nullable, [2C]): also writes [mean | E[x^2]] for a cross-replica exchange
@@ -67,5 +74,8 @@ hipError_t launch_bn_bwd_reduce(int dtype, int dz_f32, const BnBwdArgs& a, hipSt
 hipError_t launch_bn_bwd_finalize(const float* part, int rb, long M, int C, BnState st,
                                   float* dgamma, float* dbeta, hipStream_t s, int frozen = 0);
 hipError_t launch_bn_bwd_apply(int dtype, int dz_f32, const BnBwdArgs& a, hipStream_t s);
+// dual forms (16-bit or fp32 dz of the storage type, ReLU bits, no dzscale / dyhat)
+hipError_t launch_bn_bwd_reduce_dual(int dtype, const BnBwdArgs& a, hipStream_t s);
+hipError_t launch_bn_bwd_apply_dual(int dtype, const BnBwdArgs& a, hipStream_t s);
 hipError_t launch_moving_update(float* mov_mean, float* mov_var, const float* bmean,
                                 const float* bvar, int n, float decay, hipStream_t s);

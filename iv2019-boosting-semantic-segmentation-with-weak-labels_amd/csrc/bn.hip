@@ -620,6 +620,136 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwdArgs a) {
   if (base < a.M) body(base, (int)((a.M - base + L.rpp - 1) / L.rpp), std::false_type{});
 }
 
+// dual reduce: (sum dyhat, sum dyhat*xhat) for two BN layers gated by the same dz / bits, dz
+// and the bits read once; two rows in flight per thread (the second y and accumulator set
+// would push four past 256 VGPRs), rows added in order, partials in each layer's layout
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce8_dual_kernel(BnBwdArgs a) {
+  constexpr int U = 2;
+  __shared__ float sh[3][256 * 8];
+  const RowLane L = row_lane(a.C / 8);
+  const int c0 = (L.act ? L.cg : 0) * 8;
+  const long rows_per = (a.M + a.rb - 1) / a.rb;
+  const long r0 = (long)blockIdx.x * rows_per;
+  const long r1 = (r0 + rows_per < a.M) ? r0 + rows_per : a.M;
+  float s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+  if (L.act) {
+    float mu[8], inv[8], mu2[8], inv2[8];
+    ld8(a.mean, c0, mu); ld8(a.invstd, c0, inv); ld8(a.mean2, c0, mu2); ld8(a.invstd2, c0, inv2);
+    const T* DZ = (const T*)a.dz + c0;
+    const T* Y = (const T*)a.y + c0;
+    const T* Y2 = (const T*)a.y2 + c0;
+    const int cg = c0 >> 3, cgn = a.C >> 3;
+    for (long base = r0 + L.rl; base < r1; base += (long)L.rpp * U) {
+      Raw8<T> rdz[U], ry[U], ry2[U];
+      uint32_t mk[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const long m = base + k * L.rpp;
+        if (m < r1) {
+          rdz[k].load(DZ + (size_t)m * a.lddz);
+          ry[k].load(Y + (size_t)m * a.ldy);
+          ry2[k].load(Y2 + (size_t)m * a.ldy2);
+          mk[k] = a.mask[(size_t)m * cgn + cg];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if (base + k * L.rpp >= r1) continue;
+        float dz[8], y[8], y2[8];
+        rdz[k].cvt(dz); ry[k].cvt(y); ry2[k].cvt(y2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = (mk[k] >> e) & 1u ? dz[e] : 0.f;
+          s1[e] += d;
+          s2[e] += d * ((y[e] - mu[e]) * inv[e]);
+          s3[e] += d * ((y2[e] - mu2[e]) * inv2[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sh[0][threadIdx.x * 8 + e] = s1[e];
+    sh[1][threadIdx.x * 8 + e] = s2[e];
+    sh[2][threadIdx.x * 8 + e] = s3[e];
+  }
+  __syncthreads();
+  if (L.act && L.rl == 0) {
+    const int cg_b = a.C / 8 >= 256 ? 256 : a.C / 8;
+    for (int r = 1; r < L.rpp; ++r) {
+      const int t = r * cg_b + threadIdx.x;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += sh[0][t * 8 + e];
+        s2[e] += sh[1][t * 8 + e];
+        s3[e] += sh[2][t * 8 + e];
+      }
+    }
+    float* o = a.part + 2 * ((size_t)blockIdx.x * a.C + c0);
+    float* o2 = a.part2 + 2 * ((size_t)blockIdx.x * a.C + c0);
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      *(float4*)(o + 2 * e) = make_float4(s1[e], s2[e], s1[e + 1], s2[e + 1]);
+      *(float4*)(o2 + 2 * e) = make_float4(s1[e], s3[e], s1[e + 1], s3[e + 1]);
+    }
+  }
+}
+
+// dual apply: dy = scale (dyhat - sdy - xhat sdyx) for both layers from one dz / bits read
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply8_dual_kernel(BnBwdArgs a) {
+  constexpr int U = 2;
+  const RowLane L = row_lane(a.C / 8);
+  if (!L.act) return;
+  const int c0 = L.cg * 8;
+  float mu[8], inv[8], sc[8], sdy[8], sdyx[8], mu2[8], inv2[8], sc2[8], sdy2[8], sdyx2[8];
+  ld8(a.mean, c0, mu); ld8(a.invstd, c0, inv); ld8(a.scale, c0, sc);
+  ld8(a.sdy, c0, sdy); ld8(a.sdyx, c0, sdyx);
+  ld8(a.mean2, c0, mu2); ld8(a.invstd2, c0, inv2); ld8(a.scale2, c0, sc2);
+  ld8(a.sdy2, c0, sdy2); ld8(a.sdyx2, c0, sdyx2);
+  const T* DZ = (const T*)a.dz + c0;
+  const T* Y = (const T*)a.y + c0;
+  const T* Y2 = (const T*)a.y2 + c0;
+  T* DY = (T*)a.dy + c0;
+  T* DY2 = (T*)a.dy2 + c0;
+  const int cg = c0 >> 3, cgn = a.C >> 3;
+  const long step = (long)L.rpp * U;
+  for (long base = (long)blockIdx.x * step + L.rl; base < a.M; base += (long)gridDim.x * step) {
+    Raw8<T> rdz[U], ry[U], ry2[U];
+    uint32_t mk[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long m = base + k * L.rpp;
+      if (m < a.M) {
+        rdz[k].load(DZ + (size_t)m * a.lddz);
+        ry[k].load(Y + (size_t)m * a.ldy);
+        ry2[k].load(Y2 + (size_t)m * a.ldy2);
+        mk[k] = a.mask[(size_t)m * cgn + cg];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long m = base + k * L.rpp;
+      if (m >= a.M) continue;
+      float dz[8], y[8], y2[8], o[8], o2[8];
+      rdz[k].cvt(dz); ry[k].cvt(y); ry2[k].cvt(y2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = (mk[k] >> e) & 1u ? dz[e] : 0.f;
+        o[e] = sc[e] * (d - sdy[e] - ((y[e] - mu[e]) * inv[e]) * sdyx[e]);
+        o2[e] = sc2[e] * (d - sdy2[e] - ((y2[e] - mu2[e]) * inv2[e]) * sdyx2[e]);
+      }
+      BN_STORE8(T, DY + (size_t)m * a.lddy, o);
+      BN_STORE8(T, DY2 + (size_t)m * a.lddy2, o2);
+    }
+  }
+}
+
 dim3 grid8(long M, int C) {
   const int cg_n = C / 8;
   const int rpp = cg_n >= 256 ? 1 : 256 / cg_n;
@@ -799,6 +929,44 @@ hipError_t launch_bn_bwd_apply(int dtype, int dz_f32, const BnBwdArgs& a, hipStr
     return bwd_apply_t<f16_t, f16_t>(a, s);
   }
   return bwd_apply_t<float, float>(a, s);
+}
+
+template <typename T>
+bool dual_ok(const BnBwdArgs& a) {
+  return a.mask && !a.z && !a.dzscale && !a.dyhat && a.C % 8 == 0 && a.lddz % 8 == 0 &&
+         a.ldy % 8 == 0 && a.ldy2 % 8 == 0 && a.lddy % 8 == 0 && a.lddy2 % 8 == 0 &&
+         (uintptr_t)a.dz % 16 == 0;
+}
+
+hipError_t launch_bn_bwd_reduce_dual(int dtype, const BnBwdArgs& a, hipStream_t s) {
+  const int cg_n = a.C / 8;
+  const dim3 g(a.rb, cg_n > 256 ? ceil_div(cg_n, 256) : 1);
+  if (dtype == SEG_BF16) {
+    if (!dual_ok<bf16_t>(a)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_bwd_reduce8_dual_kernel<bf16_t>, g, dim3(256), 0, s, a);
+  } else if (dtype == SEG_F16) {
+    if (!dual_ok<f16_t>(a)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_bwd_reduce8_dual_kernel<f16_t>, g, dim3(256), 0, s, a);
+  } else {
+    if (!dual_ok<float>(a)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_bwd_reduce8_dual_kernel<float>, g, dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_bwd_apply_dual(int dtype, const BnBwdArgs& a, hipStream_t s) {
+  const dim3 g = grid8(a.M, a.C);
+  if (dtype == SEG_BF16) {
+    if (!dual_ok<bf16_t>(a)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_bwd_apply8_dual_kernel<bf16_t>, g, dim3(256), 0, s, a);
+  } else if (dtype == SEG_F16) {
+    if (!dual_ok<f16_t>(a)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_bwd_apply8_dual_kernel<f16_t>, g, dim3(256), 0, s, a);
+  } else {
+    if (!dual_ok<float>(a)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_bwd_apply8_dual_kernel<float>, g, dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_moving_update(float* mov_mean, float* mov_var, const float* bmean,

@@ -626,6 +626,44 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   return prof_end(c, S.s, slot);
 }
 
+// BN backward of two layers gated by the same dz / ReLU bits (a projection unit's conv3 and
+// shortcut BN): one dual reduce and one dual apply read dz and the bits once for both; each
+// layer keeps its own finalize. Batch norm, 16-bit or fp32 dz of the storage type, no
+// cross-replica exchange (that path runs the two layers through bn_backward)
+int bn_backward_dual(Step& S, int li, int li2, const Act& dz, const Act& z) {
+  seg_ctx* c = S.c;
+  ConvL& L = c->convs[li];
+  ConvL& L2 = c->convs[li2];
+  BnBwdArgs a{};
+  a.dz = dz.p; a.lddz = dz.ld; a.mask = z.mask;
+  a.y = L.y.p; a.ldy = L.y.ld; a.M = L.y.M(); a.C = L.co;
+  a.mean = L.st.mean; a.invstd = L.st.invstd; a.scale = L.st.scale;
+  a.sdy = L.st.sdy; a.sdyx = L.st.sdyx;
+  a.dy = L.dy.p; a.lddy = L.dy.ld;
+  a.part = L.bwd_part; a.rb = L.rb;
+  a.y2 = L2.y.p; a.ldy2 = L2.y.ld;
+  a.mean2 = L2.st.mean; a.invstd2 = L2.st.invstd; a.scale2 = L2.st.scale;
+  a.sdy2 = L2.st.sdy; a.sdyx2 = L2.st.sdyx;
+  a.dy2 = L2.dy.p; a.lddy2 = L2.dy.ld;
+  a.part2 = L2.bwd_part;
+  const double esz = seg_half(S.dt) ? 2.0 : 4.0;
+  const double me = a.M * (double)a.C * 1e-9;
+  const double gb_in = me * (esz + 0.125 + 2 * esz);   // dz + bits + both y
+  int slot;
+  if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
+  HIPCALL(c, launch_bn_bwd_reduce_dual(S.dt, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
+  const bool tb = c->cfg.train_bn != 0;
+  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st, tb ? c->grads + L.g_off : nullptr,
+                                    tb ? c->grads + L.b_off : nullptr, S.s, c->bn_infer));
+  HIPCALL(c, launch_bn_bwd_finalize(L2.bwd_part, L2.rb, a.M, L2.co, L2.st,
+                                    tb ? c->grads + L2.g_off : nullptr,
+                                    tb ? c->grads + L2.b_off : nullptr, S.s, c->bn_infer));
+  if (int r = prof_begin(c, S.s, 5, li, gb_in + me * 2 * esz, &slot)) return r;
+  HIPCALL(c, launch_bn_bwd_apply_dual(S.dt, a, S.s));
+  return prof_end(c, S.s, slot);
+}
+
 // group norm backward (gn.h): per image the batch-norm reduce (S1, S2 per channel) into
 // its slice of the partials, one finalize for the layer (dgamma / dbeta, per-image group
 // means), per image the batch-norm apply with scale = invstd and the gradient times gamma
@@ -1169,9 +1207,16 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
   // (dpre), the residual of the unit's input gradient. (Measured and rejected: folding the
   // mask into conv1's dgrad epilogue instead, 1.8 % slower per step.)
   const Act* dpre = u.kind != SC_CONV ? &u.dpre : nullptr;
-  if (int r = bn_backward(S, u.c3, u.dout, 0, &u.out, dpre)) return r;
-  if (u.kind == SC_CONV)
-    if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
+  const ConvL& L3 = c->convs[u.c3];
+  const ConvL& Ls = c->convs[u.kind == SC_CONV ? u.sc : u.c3];
+  if (u.kind == SC_CONV && !c->gn && !c->sync_fn && u.out.mask && u.out.C == L3.co &&
+      Ls.co == L3.co && Ls.rb == L3.rb && Ls.y.M() == L3.y.M()) {
+    if (int r = bn_backward_dual(S, u.c3, u.sc, u.dout, u.out)) return r;
+  } else {
+    if (int r = bn_backward(S, u.c3, u.dout, 0, &u.out, dpre)) return r;
+    if (u.kind == SC_CONV)
+      if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
+  }
   if (int r = conv_wgrad(S, u.c3, u.z2)) return r;
   if (int r = conv_dgrad(S, u.c3, u.dz2)) return r;
   if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr)) return r;
