@@ -1527,12 +1527,15 @@ int seg_create(int device, const seg_cfg* cfg, seg_ctx** out) {
 int seg_destroy(seg_ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
+  if (c->side) (void)hipStreamSynchronize(c->side);   // a deferred stem weight gradient
+  (void)hipDeviceSynchronize();
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->infer_jobs) (void)hipFree(c->infer_jobs);
   for (auto ev : c->prof.ev) (void)hipEventDestroy(ev);
   for (auto ev : c->bk_ev) (void)hipEventDestroy(ev);
   for (auto ev : c->ev_dy) (void)hipEventDestroy(ev);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->ev_prestem) (void)hipEventDestroy(c->ev_prestem);
   if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
   return 0;
@@ -1911,6 +1914,8 @@ int seg_prepare_labels(const uint8_t* raw, int n, int src_h, int src_w, int H, i
 
 int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* ld, int* dtype) {
   if (!c || !name) return set_err(c ? &c->err : nullptr, -EINVAL, "null argument");
+  if (c->stem_pending)   // the caller reads on its own stream: a deferred stem gradient first
+    HIPCALL(c, hipEventSynchronize(c->ev_join));
   std::string n(name);
   Act a;
   int dt = c->dt == SEG_BF16 ? SEG_DTYPE_BF16 : (c->dt == SEG_F16 ? SEG_DTYPE_F16 : SEG_DTYPE_F32);
