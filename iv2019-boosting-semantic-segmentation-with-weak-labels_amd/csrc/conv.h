@@ -28,6 +28,13 @@ struct ConvArgs {
   float* stats;   // BN partials [mtiles][Co] x {sum, M2} (nullptr = none)
   int tap8;       // tap mode: a tap is tap8 16-B chunks of K (2: the space-to-depth stem, 16
                   // channels per tap); K = KH*KW*C is padded to a multiple of 64 with zero weights
+  // K-concatenated second GEMM (ping-pong dense 1x1 path only): y = x w^T + x2 w2^T, x2 [..][ldx2]
+  // with C2 channels on the same pixels, w2 [Co][ldw2]; a projection unit's conv1 + shortcut
+  // data gradients into the unit input in one accumulation (x2 = nullptr: single GEMM)
+  const void* x2;
+  int ldx2, C2;
+  const void* w2;
+  int ldw2;
 };
 
 struct WgradArgs {

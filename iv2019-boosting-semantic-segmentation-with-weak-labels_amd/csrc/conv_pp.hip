@@ -106,7 +106,11 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   tile_of(tile, mt, nt);
   long m0 = (long)mt * BM;
   int n0 = nt * BN;
-  const int nk = (a.KH * a.KW * a.C) / PBK;
+  // ST == 4: the dense 1x1 path of ST == 0 plus a K-concatenated second GEMM (x2, w2) whose
+  // K-tiles follow the first's (a separate instantiation: the extra addressing state cost the
+  // plain 1x1 launches 4 % when it was a runtime branch of ST == 0)
+  constexpr bool dual = ST == 4;
+  const int nk = (a.KH * a.KW * a.C) / PBK + (dual ? a.C2 / PBK : 0);
   const int ntaps = a.KH * a.KW;
   const E* X = (const E*)a.x;
   const E* Wt = (const E*)a.w;
@@ -119,6 +123,11 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   const auto rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0,
                                                       (int)((long)a.N * a.H * a.W * a.ldx * 2), 0x00020000);
   const auto rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (int)((long)a.Co * a.ldw * 2), 0x00020000);
+  const auto rs_x2 = dual ? __builtin_amdgcn_make_buffer_rsrc((void*)a.x2, (short)0,
+                                                              (int)((long)a.N * a.H * a.W * a.ldx2 * 2), 0x00020000)
+                          : rs_x;
+  const auto rs_w2 = dual ? __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, (int)((long)a.Co * a.ldw2 * 2), 0x00020000)
+                          : rs_w;
   // A rows: half h, DMA instruction i -> tile row h*128 + (i*8+wave)*8 + lane/8 (j = h*2 + i).
   // ST == 1: byte offset of the tap-(0,0) source and a validity mask, bit kh (0-3) for the row
   // and bit 4+kw for the column of every tap; ST == 2 (transposed gather) decodes per tap.
@@ -126,6 +135,8 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   int a_voff[4], a_bits[4], a_h0[4], a_w0[4], a_lc[4];
   long a_nb[4];
   uint32_t b_voff[4];
+  int a_voff2[4];        // dual: the same rows of x2
+  uint32_t b_voff2[4];   // dual: the same output channels of w2
   auto setup_lanes = [&](long m0_, int n0_) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -138,10 +149,11 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       // the per-tile setup on short-K layers
       const int m = (int)m0_ + row;
       const bool ok = m < (int)M;
-      if constexpr (ST == 0) {
+      if constexpr (ST == 0 || ST == 4) {
         // 1x1, stride 1, no padding (H x W = Ho x Wo): the source row IS pixel m, every tap
         // valid; no pixel decode (the divisions were ~2.5k cycles of the per-tile setup)
         a_voff[j] = (ok ? m : 0) * a.ldx * 2 + a_lc[j] * 16;
+        a_voff2[j] = dual ? (ok ? m : 0) * a.ldx2 * 2 + a_lc[j] * 16 : 0;
         a_bits[j] = ok ? 0x11 : 0;
         continue;
       }
@@ -169,19 +181,22 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       const int rr = ((j & 1) * 8 + wave) * 8 + (lane >> 3);
       const int co = n0_ + (j >> 1) * 128 + rr;
       b_voff[j] = co < a.Co ? (uint32_t)((co * a.ldw + swz(rr, pc) * 8) * 2) : OOB;
+      b_voff2[j] = dual && co < a.Co ? (uint32_t)((co * a.ldw2 + swz(rr, pc) * 8) * 2) : OOB;
     }
   };
   setup_lanes(m0, n0);
 
   // per-K-tile wave-uniform decode. K-tile order: channel chunk outer, tap inner, so the
   // KH*KW shifted reads of one chunk's source rows follow each other while they are in L2
-  struct KT { int need, s_tap2, k02, dh, dw, c0; };
-  int nx_tap = 0, nx_c0 = 0;   // (tap, chunk) of the next K-tile to decode, stepped in order
+  struct KT { int need, s_tap2, k02, dh, dw, c0, sec; };
+  int nx_tap = 0, nx_c0 = 0, nx_sec = 0;   // (tap, chunk, GEMM) of the next K-tile to decode
   auto ktile_next = [&]() {
     KT t;
     const int tap = nx_tap;
     t.c0 = nx_c0;
+    t.sec = nx_sec;
     if (++nx_tap == ntaps) { nx_tap = 0; nx_c0 += PBK; }
+    if (dual && nx_sec == 0 && nx_c0 == a.C) { nx_sec = 1; nx_c0 = 0; }
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     t.dh = kh * a.dil;
     t.dw = kw * a.dil;
@@ -200,7 +215,12 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       if (hid < 2) {
         const int j = hid * 2 + i;
         uint32_t off;
-        if constexpr (ST <= 1) {
+        if (dual && t.sec) {   // wave-uniform: the second GEMM's A rows (dense 1x1)
+          off = a_bits[j] ? (uint32_t)(a_voff2[j] + t.s_tap2) : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x2, ldst, 16, off, 0, 0, 0);
+          continue;
+        }
+        if constexpr (ST <= 1 || ST == 4) {
           off = (a_bits[j] & t.need) == t.need ? (uint32_t)(a_voff[j] + t.s_tap2) : OOB;
         } else {
           int hi = a_h0[j] + t.dh, wi = a_w0[j] + t.dw;
@@ -213,7 +233,8 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, ldst, 16, off, 0, 0, 0);
       } else {
         const int j = (hid - 2) * 2 + i;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, ldst, 16, b_voff[j] + t.k02, 0, 0, 0);
+        if (dual && t.sec) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w2, ldst, 16, b_voff2[j] + t.k02, 0, 0, 0);
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, ldst, 16, b_voff[j] + t.k02, 0, 0, 0);
       }
     }
   };
@@ -257,6 +278,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   auto prologue = [&]() {
     nx_tap = 0;
     nx_c0 = 0;
+    nx_sec = 0;
     const KT t0 = ktile_next();
     issue_half(0, t0, 0);
     issue_half(0, t0, 2);
@@ -576,14 +598,19 @@ bool conv_nt_pp_ok(const ConvArgs& a) {
   return !a.tap8 && a.Co > 128 && a.Co % 8 == 0 && a.ldy % 8 == 0 &&
          a.KH <= 4 && a.KW <= 4 && conv_nt_v2_ok(a) &&
          (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31) && (long)a.Co * a.ldw * 2 < (1L << 31) &&
-         (long)a.N * a.Ho * a.Wo < (1L << 31);   // 32-bit pixel indices
+         (long)a.N * a.Ho * a.Wo < (1L << 31) &&   // 32-bit pixel indices
+         (!a.x2 || (a.KH == 1 && a.KW == 1 && a.st == 1 && a.sf == 1 && a.pad_h == 0 && a.pad_w == 0 &&
+                    a.H == a.Ho && a.W == a.Wo && a.C % 64 == 0 && a.C2 % 64 == 0 && a.ldx2 % 8 == 0 &&
+                    a.ldw2 % 8 == 0 && (long)a.N * a.H * a.W * a.ldx2 * 2 < (1L << 31) &&
+                    (long)a.Co * a.ldw2 * 2 < (1L << 31) && !a.r && !a.r2));
 }
 
 template <typename E>
 hipError_t nt_pp_e(const ConvArgs& a, hipStream_t s) {
   if (a.st == 1 && a.KH == 1 && a.KW == 1 && a.sf == 1 && a.pad_h == 0 && a.pad_w == 0 &&
       a.H == a.Ho && a.W == a.Wo)
-    return pp_launch_st<E, 0>(a, s);   // dense 1x1 rows
+    return a.x2 ? pp_launch_st<E, 4>(a, s)    // dense 1x1 rows + the second GEMM
+                : pp_launch_st<E, 0>(a, s);   // dense 1x1 rows
   if (a.st == 1) return pp_launch_st<E, 1>(a, s);
   if (a.st == 2) return pp_launch_st<E, 2>(a, s);
   return hipErrorInvalidValue;

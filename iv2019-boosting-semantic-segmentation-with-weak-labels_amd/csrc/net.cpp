@@ -736,6 +736,31 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
   return prof_end(c, S.s, slot);
 }
 
+// dx = dgrad(li) + dgrad(li2) in one K-concatenated ping-pong launch: a projection unit's conv1
+// and shortcut (both 1 x 1, stride 1, the unit input's geometry). Returns 1 when the shapes do
+// not fit that path (the caller then runs the two data gradients with the residual add)
+int conv_dgrad_dual(Step& S, int li, int li2, const Act& dx) {
+  seg_ctx* c = S.c;
+  const ConvL& L = c->convs[li];
+  const ConvL& L2 = c->convs[li2];
+  if (!seg_half(S.dt) || L.k != 1 || L2.k != 1 || L.stride != 1 || L2.stride != 1 ||
+      L.ci != L2.ci || L.Ho != L2.Ho || L.Wo != L2.Wo || L.H != L.Ho || L.W != L.Wo ||
+      !L.wt_lp || !L2.wt_lp)
+    return 1;
+  ConvArgs a = dgrad_args(c, li, dx, nullptr, nullptr);
+  a.x2 = L2.dy.p; a.ldx2 = L2.dy.ld; a.C2 = L2.co;
+  a.w2 = L2.wt_lp; a.ldw2 = L2.co;
+  if (a.st != 1 || a.sf != 1 || a.pad_h || a.pad_w || !conv_nt_pp_ok(a)) return 1;
+  const long M = (long)L.N * L.H * L.W;
+  const double gbx = ((double)M * (L.co + L2.co) + (double)(L.co + L2.co) * L.ci + (double)M * L.ci) *
+                     c->esz * 1e-9;
+  int slot;
+  if (int r = prof_begin(c, S.s, 1, li, 2.0 * M * L.ci * (L.co + L2.co) * 1e-9, &slot, gbx)) return r;
+  HIPCALL(c, launch_conv_nt_pp(S.dt, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
+  return 0;
+}
+
 ConvArgs dgrad_args(seg_ctx* c, int li, const Act& dx, const Act* r1, const Act* r2) {
   ConvL& L = c->convs[li];
   ConvArgs a{};
@@ -1235,10 +1260,15 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
                                     u.dpre.W, u.dpre.C, u.dpre.ld, u.stride, S.s));
       return 0;
     }
-    case SC_CONV:
+    case SC_CONV: {
       if (int r = conv_wgrad(S, u.sc, u.in)) return r;
+      if (!accumulate) {   // one K-concatenated GEMM when both are 1 x 1 stride-1 ping-pong shapes
+        const int r = conv_dgrad_dual(S, u.c1, u.sc, dx);
+        if (r <= 0) return r;
+      }
       if (int r = conv_dgrad(S, u.c1, dx, accumulate ? &dx : nullptr)) return r;
       return conv_dgrad(S, u.sc, dx, &dx);
+    }
   }
   return 0;
 }
