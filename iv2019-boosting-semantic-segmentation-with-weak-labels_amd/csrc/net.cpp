@@ -1957,6 +1957,7 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
   else if (n == "dfeat") a = c->dfeat;
   else if (n == "z0") {   // stem BN + ReLU output (the max-pool input)
     if (c->z0_stale) {   // fused forward: materialise it (same kernel, this step's statistics)
+      HIPCALL(c, hipDeviceSynchronize());   // the step's streams may be non-blocking
       Step S{c, nullptr, c->dt};
       if (int r = bn_apply(S, c->stem, c->z0, 0)) return r;
       HIPCALL(c, hipStreamSynchronize(nullptr));
