@@ -59,36 +59,83 @@ CLS_NAMES_F32 = {0: "conv_nt_kernel (fp32 MFMA forward)", 1: "conv_nt_kernel (fp
 EMA_DECAY = 0.9   # utils/utils.py:112 default; off when distributed (system_factory.py:236-238)
 
 
-def cpu_baseline(threads, pyramid):
-    """Oracle (PyTorch-CPU fp32 restatement of the TF semantics) on a bounded sample:
-    one 1024x2048 image, one full training step, after a 256x512 warm-up; plus the C1 shape
-    (the reference's own CPU configuration: R50, no pyramid, 512 x 1024, batch 2, one step)."""
-    import numpy as np
+def host_cpu_info():
+    """Host CPU facts reported beside the CPU baseline: logical CPUs, the affinity set this
+    process may run on, the cgroup v2 CPU quota (None = unlimited) and the CPU model."""
+    info = {"cpu_count": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = None
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpu_quota"] = quota
+    model, sockets = None, set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name") and model is None:
+                model = line.split(":", 1)[1].strip()
+            elif line.startswith("physical id"):
+                sockets.add(line.split(":", 1)[1].strip())
+    except OSError:
+        pass
+    info["cpu_model"] = model
+    info["sockets"] = len(sockets) or None
+    return info
+
+
+def baseline_threads(info):
+    """Threads for the CPU baseline: every core this process may use. On the GPU box that is the
+    cgroup CPU quota (16 of the 256 logical CPUs); more threads than the quota only contend for
+    it (profiles/r03_cpu_threads.txt: the C1 step takes 6.3 s on 16, 7.7 s on 32, 11.0 s on 64)."""
+    n = info.get("affinity") or info.get("cpu_count") or 1
+    if info.get("cgroup_cpu_quota"):
+        n = min(n, max(1, int(info["cgroup_cpu_quota"])))
+    return n
+
+
+def cpu_baseline(pyramid, reps=3):
+    """Oracle (PyTorch-CPU fp32 restatement of the TF semantics) on the host cores, as SURVEY
+    §8(d) / BASELINE.md plan it: one warm-up step at the timed shape, then the median of `reps`
+    full training steps (fwd + loss + bwd + SGDM), at 1024x2048 batch 1 (the metric's image) and
+    at C1 (the reference's own CPU configuration: R50, no pyramid, 512x1024, batch 2)."""
+    import statistics
     import torch
     from input_pipelines.synthetic import batch
     from oracle.tfseg import OracleNet, SegConfig, init_params
+    info = host_cpu_info()
+    threads = baseline_threads(info)
     torch.set_num_threads(threads)
-    warm = SegConfig(height=256, width=512, nb_pp=1, pyramid=pyramid)
-    d = batch(1, 1, 0, 0, 256, 512)
-    OracleNet(warm, init_params(warm), dtype=torch.float32).train_step(d["images"], d["px"])
+
+    def timed(cfg, d):
+        net = OracleNet(cfg, init_params(cfg), dtype=torch.float32)
+        net.train_step(d["images"], d["px"])          # warm-up at the timed shape
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            net.train_step(d["images"], d["px"])
+            ts.append(time.perf_counter() - t)
+        return statistics.median(ts), ts
+
     cfg = SegConfig(height=H, width=W, nb_pp=1, pyramid=pyramid)
-    net = OracleNet(cfg, init_params(cfg), dtype=torch.float32)
-    d = batch(2, 1, 0, 0, H, W)
-    t = time.perf_counter()
-    net.train_step(d["images"], d["px"])
-    dt = time.perf_counter() - t
-    del net
+    dt, ts = timed(cfg, batch(2, 1, 0, 0, H, W))
     c1 = SegConfig(height=512, width=1024, nb_pp=2, pyramid="none")
-    net = OracleNet(c1, init_params(c1), dtype=torch.float32)
-    d = batch(3, 2, 0, 0, 512, 1024)
-    t = time.perf_counter()
-    net.train_step(d["images"], d["px"])
-    d1 = time.perf_counter() - t
+    d1, ts1 = timed(c1, batch(3, 2, 0, 0, 512, 1024))
     return {"value": round(1.0 / dt, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"1 image 1024x2048, 1 full step (fwd+loss+bwd+SGDM), R50+{pyramid.upper()}, fp32, "
-                      f"oracle/tfseg.py on {threads} host threads ({dt:.1f} s)",
+            "cpu_model": info["cpu_model"], "cpu_count": info["cpu_count"],
+            "cgroup_cpu_quota": info["cgroup_cpu_quota"], "sockets": info["sockets"],
+            "sample": f"1 image 1024x2048, median of {reps} full steps (fwd+loss+bwd+SGDM) after "
+                      f"1 warm-up step at that shape, R50+{pyramid.upper()}, fp32, oracle/tfseg.py "
+                      f"(PyTorch CPU) on {threads} threads; steps " +
+                      ", ".join(f"{t:.1f}" for t in ts) + " s",
             "c1": {"value": round(2.0 / d1, 4), "unit": "images/sec",
-                   "sample": f"C1: R50 (no pyramid) 512x1024 batch 2, 1 full step, fp32 ({d1:.1f} s)"}}
+                   "sample": f"C1: R50 (no pyramid) 512x1024 batch 2, median of {reps} steps after 1 "
+                             "warm-up; steps " + ", ".join(f"{t:.1f}" for t in ts1) + " s"}}
 
 
 def main():
@@ -343,7 +390,7 @@ def main():
               "what": "moving-statistics BN forward + seg_predict + confusion (3 batches)"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C2":
-        cpu = cpu_baseline(threads=min(16, os.cpu_count() or 1), pyramid=args.pyramid)
+        cpu = cpu_baseline(pyramid=args.pyramid)
 
     if rank == 0:
         value = world * NB * args.steps / elapsed

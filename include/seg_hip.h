@@ -181,8 +181,9 @@ int seg_found_inf(seg_ctx* ctx, const int32_t** flag_device);
  * mean(dyhat * xhat)] so dx is the gradient through the global statistics. `allreduce` must
  * SUM `n` floats at the device pointer `buf` in place across the `world` replicas, ordered
  * on `stream` (e.g. torch.distributed.all_reduce on that stream, RCCL or gloo), and return 0;
- * a nonzero return fails the step. fn = NULL (or world = 1) turns synchronisation off. */
-typedef int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, hipStream_t stream);
+ * a nonzero return fails the step. fn = NULL turns synchronisation off; world = 1 with a hook
+ * still calls it (a one-replica exchange: the sync-BN arithmetic over one replica). */
+typedef int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, void* stream);
 int seg_set_bn_sync(seg_ctx* ctx, seg_allreduce_fn allreduce, void* user, int world);
 
 /* gradient all-reduce buckets, in the order the backward completes them: n buckets

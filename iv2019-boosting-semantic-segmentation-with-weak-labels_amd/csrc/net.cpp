@@ -1506,11 +1506,13 @@ int refresh_stem_pad(seg_ctx* c, hipStream_t s) {
 }
 
 // a deferred stem weight gradient (seg_set_defer_stem) must be complete before anything else
-// on stream s reads or rewrites the step's buffers
-int join_stem(seg_ctx* c, hipStream_t s) {
+// on stream s reads or rewrites the step's buffers. The pending state is kept until the
+// gradient is consumed (seg_apply_update) or superseded (seg_backward): a join on another
+// stream must not let a later seg_apply_update skip its own join
+int join_stem(seg_ctx* c, hipStream_t s, bool consume = false) {
   if (!c->stem_pending) return 0;
-  c->stem_pending = false;
   HIPCALL(c, hipStreamWaitEvent(s, c->ev_join, 0));
+  if (consume) c->stem_pending = false;
   return 0;
 }
 
@@ -1534,10 +1536,11 @@ int seg_set_loss_scale(seg_ctx* c, float scale);
 int seg_create(int device, const seg_cfg* cfg, seg_ctx** out) {
   if (!cfg || !out) return set_err(nullptr, -EINVAL, "null argument");
   *out = nullptr;
-  hipError_t e = hipSetDevice(device);
-  if (e != hipSuccess) return set_err(nullptr, -ENODEV, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+  // host-side validation first: a bad configuration fails the same way with or without a GPU
   if (cfg->dtype < SEG_DTYPE_F32 || cfg->dtype > SEG_DTYPE_F16)
     return set_err(nullptr, -EINVAL, "dtype %d (SEG_DTYPE_F32 / _BF16 / _F16)", cfg->dtype);
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return set_err(nullptr, -ENODEV, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
   seg_ctx* c = new seg_ctx();
   c->cfg = *cfg;
   c->device = device;
@@ -1730,7 +1733,7 @@ int seg_full_predictions(seg_ctx* c, float* logits_out, float* probs_out,
 int seg_backward(seg_ctx* c, void* stream) {
   NEED_BOUND(c);
   Step S{c, (hipStream_t)stream, c->dt};
-  if (int r = join_stem(c, S.s)) return r;
+  if (int r = join_stem(c, S.s, true)) return r;
   return backward(S);
 }
 
@@ -1746,7 +1749,7 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
   const bool split = c->stem_pending && !c->skip_flag && grad_scale == 1.f && !stl.wt_lp &&
                      st_hi <= c->n_decay;
   if (!split)
-    if (int r = join_stem(c, s)) return r;
+    if (int r = join_stem(c, s, true)) return r;
   if (c->skip_flag) {   // loss-scaled (fp16) step: unscale, and skip it if anything overflowed
     HIPCALL(c, hipMemsetAsync(c->skip_flag, 0, sizeof(int), s));
     HIPCALL(c, launch_nonfinite(c->grads, c->n_train, c->skip_flag, s));
@@ -1805,7 +1808,7 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
                                     c->grads + c->n_train + half, (int)half, c->cfg.bn_decay, s));
   if (c->n_flip) HIPCALL(c, launch_weight_flip_batched(c->dt, c->flip_jobs, c->n_flip, c->flip_total, s));
   if (split) {   // the stem's weight gradient is done: its update, then the regulariser sum
-    if (int r = join_stem(c, s)) return r;
+    if (int r = join_stem(c, s, true)) return r;
     HIPCALL(c, launch_sgdm(st_a, s));
     HIPCALL(c, launch_sum_partials(c->reg_part, nparts, c->reg_out, s));
   }
@@ -1859,7 +1862,7 @@ int seg_set_bn_sync(seg_ctx* c, seg_allreduce_fn fn, void* user, int world) {
   if (c->gn && fn && world > 1)   // module_arg_scope :329-331
     return set_err(&c->err, -EINVAL, "cross_replica_norm is supported only for batch normalization");
   if (world < 1) return set_err(&c->err, -EINVAL, "world must be >= 1");
-  if (!fn || world == 1) {
+  if (!fn) {   // world == 1 with a hook still exchanges (a one-replica collective)
     c->sync_fn = nullptr;
     c->sync_user = nullptr;
     c->sync_world = 1;
@@ -1983,6 +1986,7 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
         if (int r = dalloc(c, &p, (size_t)st.N * st.H * st.W * 8 * 2)) return r;
         c->img_dbg = p;
       }
+      HIPCALL(c, hipDeviceSynchronize());   // the s2d image is written on the step's stream
       HIPCALL(c, launch_unshuffle_s2d(c->img.p, c->img_dbg, st.N, st.H, st.W, c->img.H, c->img.W,
                                       st.pad_h, st.pad_w, 0));
       HIPCALL(c, hipDeviceSynchronize());

@@ -44,7 +44,7 @@ def world_size():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
-def allreduce_grads(ctx, overlap=True):
+def allreduce_grads(ctx, overlap=True, always=False):
     """SUM all-reduce of the flat gradient buffer (gradients + BN batch-statistics tail) over
     the process group (RCCL over xGMI on MI355X; gloo on CPU tests). Returns the scale that
     turns the sum into the tower mean (applied inside the fused update).
@@ -53,11 +53,12 @@ def allreduce_grads(ctx, overlap=True):
     in the order the backward writes them, then the BN tail) on a side stream, each
     collective waiting only for its bucket's event, so the all-reduce of the head and upper
     layers overlaps the backward of the lower ones; the compute stream waits for the side
-    stream before the update."""
+    stream before the update. `always` runs the collective even in a one-rank group (tests
+    of the RCCL path on one GPU); otherwise a single rank skips it."""
     import torch
     import torch.distributed as dist
     n = world_size()
-    if n <= 1:
+    if n <= 1 and not (always and dist.is_available() and dist.is_initialized()):
         return 1.0
     buckets = ctx.grad_buckets() if overlap and hasattr(ctx, 'grad_buckets') else None
     if buckets and ctx.grads.is_cuda:

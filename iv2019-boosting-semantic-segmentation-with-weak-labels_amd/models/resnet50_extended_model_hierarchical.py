@@ -140,7 +140,15 @@ class Predictions(MutableMapping):
     ``_context``. The nine full-resolution entries of LAZY_KEYS are produced together by one
     ``seg_full_predictions`` launch on first access (f32 [N, H, W, c] logits and
     probabilities, int32 [N, H, W] decisions); reading them after the context has run another
-    forward raises instead of returning the newer forward's values."""
+    forward raises instead of returning the newer forward's values.
+
+    Cost of generic iteration: the key set is the reference's (iteration lists the lazy keys
+    too, so ``set(predictions)`` matches the reference dict), which means ``dict(predictions)``,
+    ``.items()`` or ``.values()`` materialise the full-resolution outputs — about
+    2·N·H·W·(c1+c2+c3)·4 bytes (4.7 GB for Vistas at 1024x2048, N = 4) — on every batch.
+    Consumers that need only the decisions read ``predictions['decisions']`` (the PREDICT loop
+    of ``SemanticSegmentation.predict`` and ``predict.py`` do), or ``materialised()`` for the
+    entries computed so far without a launch."""
 
     def __init__(self, ctx, dataset='cityscapes'):
         import torch

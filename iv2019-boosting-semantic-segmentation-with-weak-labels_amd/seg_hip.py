@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = [
     "seg_crc32c", "seg_prepare_images", "seg_prepare_labels",
 ]
 
-# int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, hipStream_t stream)
+# int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, void* stream)
 SEG_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                     ctypes.c_void_p)
 
@@ -300,16 +300,18 @@ class SegContext:
         check(LIB.seg_found_inf(self.h, ctypes.byref(p)), self.h)
         return None if not p.value else _wrap_i32(p.value, (1,), self.device)
 
-    def set_bn_sync(self, world=None, group=None):
+    def set_bn_sync(self, world=None, group=None, always=False):
         """Cross-replica batch norm (the reference's --cross_replica_norm, see seg_set_bn_sync):
         each BN layer's moments (forward) and gradient means (backward) are summed over
         `group` by torch.distributed.all_reduce (RCCL or gloo) ordered on the step's stream.
-        world=None takes the group's size; a world of 1 turns synchronisation off."""
+        world=None takes the group's size; a world of 1 turns synchronisation off unless
+        `always` (then the one-replica group still runs every exchange: tests of the
+        collective path on one GPU)."""
         import torch
         import torch.distributed as dist
         if world is None:
             world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
-        if world <= 1:
+        if world <= 1 and not always:
             check(LIB.seg_set_bn_sync(self.h, SEG_ALLREDUCE_FN(), None, 1), self.h)
             self._sync_cb = None
             return

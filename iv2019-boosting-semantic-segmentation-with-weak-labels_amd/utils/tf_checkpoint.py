@@ -25,6 +25,7 @@ from __future__ import annotations
 import ctypes
 import os
 import struct
+import warnings
 from typing import Dict, Iterable, List, Tuple
 
 import numpy as np
@@ -426,14 +427,26 @@ def import_checkpoint(ctx, prefix: str, momentum: bool = True, restore_emas: boo
         raise KeyError(f'{len(missing)} variables missing from {prefix}: {missing[:3]}')
     ctx.load_params({p.name: _native_layout(p, vals[src(p)]) for p in ctx.param_info})
 
-    def fill(buf, key):
+    def fill(buf, *keys):
+        hit = 0
         for p in ctx.param_info:
-            v = vals.get(key(p.name))
-            if v is not None and p.kind not in ('moving_mean', 'moving_variance'):
+            if p.kind in ('moving_mean', 'moving_variance'):
+                continue
+            v = next((vals[k(p.name)] for k in keys if k(p.name) in vals), None)
+            if v is not None:
+                hit += 1
                 buf[p.offset:p.offset + p.numel].copy_(
                     torch.as_tensor(_native_layout(p, v).reshape(-1).astype(np.float32)))
+        return hit
     if momentum:
-        fill(ctx.momentum, lambda n: n + '/Momentum')
+        # the reference builds its optimizer inside variable_scope('train_ops')
+        # (define_estimator_hierarchical.py:114-117), so its slots may carry that prefix; the
+        # slot name is not pinned by any reference artefact (parity unpinned): accept both
+        n_slots = fill(ctx.momentum, lambda n: n + '/Momentum', lambda n: 'train_ops/' + n + '/Momentum')
+        n_train = sum(p.kind not in ('moving_mean', 'moving_variance') for p in ctx.param_info)
+        if n_slots == 0 and n_train:
+            warnings.warn(f'{prefix}: no Momentum slot found for {n_train} trainable variables; '
+                          'training resumes with zero momentum')
         if ctx.ema is not None:   # after load_params, which reset the shadows to the weights
             fill(ctx.ema, ema_name)
     return int(vals.get('global_step', 0))

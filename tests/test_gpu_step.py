@@ -245,6 +245,44 @@ def test_defer_stem_update_matches(cuda, dtype):
     assert np.allclose(r0, r1, rtol=1e-6), (r0, r1)
 
 
+def test_defer_stem_join_on_other_stream(cuda):
+    """with defer on, a join-taking call on another stream (seg_predict on B) between
+    seg_backward and seg_apply_update (both on A) must not consume the pending stem join: the
+    update on A still waits for the stem's weight gradient. Bitwise against the joined update."""
+    from input_pipelines.synthetic import batch
+    from seg_hip import SegContext
+    cfg = SegConfig(height=256, width=512, nb_pp=1, nb_pb=1, pyramid="psp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=12).items()}
+    data = batch(22, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
+    img = torch.as_tensor(data["images"]).to(cuda)
+    px = torch.as_tensor(data["px"]).to(cuda)
+    bb = torch.as_tensor(data["bbox"]).to(cuda)
+    dec = torch.empty((2, cfg.height, cfg.width), dtype=torch.int32, device=cuda)
+    out = []
+    for defer in (False, True):
+        a, b = torch.cuda.Stream(cuda), torch.cuda.Stream(cuda)
+        ctx = SegContext(pyramid=cfg.pyramid, height=cfg.height, width=cfg.width, nb_pp=1, nb_pb=1,
+                         dtype="bf16")
+        ctx.load_params(params)
+        ctx.set_defer_stem(defer)
+        a.wait_stream(torch.cuda.current_stream(cuda))
+        for _ in range(2):
+            ctx.forward(img, stream=a)
+            ctx.loss(px, bb, None, stream=a)
+            ctx.backward(stream=a)
+            b.wait_stream(a)
+            ctx.predict(list(range(19)) + [-1], dec, stream=b)
+            ctx.apply_update(0.01, 0.9, stream=a)
+            a.wait_stream(b)
+        torch.cuda.synchronize()
+        out.append((ctx.named("params"), ctx.momentum.cpu().numpy().copy()))
+        ctx.close()
+    (p0, m0), (p1, m1) = out
+    for k in p0:
+        assert np.array_equal(p0[k], p1[k]), k
+    assert np.array_equal(m0, m1)
+
+
 @pytest.mark.parametrize("nesterov", [False, True], ids=["momentum", "nesterov"])
 def test_two_step_fp32(cuda, nesterov):
     """Step 2 starts from the native step-1 state: its forward (losses, logits) matches the
