@@ -158,6 +158,14 @@ int seg_prepare_images(const uint8_t* raw, int n, int src_h, int src_w, int H, i
                        void* stream);
 int seg_prepare_labels(const uint8_t* raw, int n, int src_h, int src_w, int H, int W,
                        const int32_t* lids2cids, int n_lids, int32_t* out, void* stream);
+/* seg_prepare_images_crop: the weak-label streams' image path (resize_images_and_labels with
+ *   preserve_aspect_ratio, input_pipelines/utils.py:181-241, under the OpenImages train inputs,
+ *   input_subset_bboxes_v2.py:111-125): convert_image_dtype -> bilinear resize (align_corners =
+ *   False) to resized_h x resized_w -> the H x W window at (crop_y, crop_x) -> from_0_1_to_m1_1.
+ *   Only the window is computed; bitwise the same values as resizing and slicing. */
+int seg_prepare_images_crop(const uint8_t* raw, int n, int src_h, int src_w, int resized_h,
+                            int resized_w, int crop_y, int crop_x, int H, int W, float* out,
+                            void* stream);
 
 /* checkpoint interop (define_initializers.py:72-131, define_savers.py:38-66): CRC-32C of
  * host bytes, continuing from `crc` (0 to start) — the checksum TF tensor bundles

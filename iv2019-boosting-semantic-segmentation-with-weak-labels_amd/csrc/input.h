@@ -14,7 +14,8 @@
 
 struct LidMap { int n; int cid[SEG_MAX_LIDS]; };
 
-hipError_t launch_prepare_images(const uint8_t* raw, int n, int Hr, int Wr, int H, int W,
-                                 float* out, hipStream_t s);
+// resized to Hs x Ws, then the H x W window at (cy, cx) (plain resize: Hs = H, Ws = W, 0, 0)
+hipError_t launch_prepare_images(const uint8_t* raw, int n, int Hr, int Wr, int Hs, int Ws,
+                                 int cy, int cx, int H, int W, float* out, hipStream_t s);
 hipError_t launch_prepare_labels(const uint8_t* raw, int n, int Hr, int Wr, int H, int W,
                                  const LidMap& m, int32_t* out, hipStream_t s);

@@ -21,9 +21,13 @@ __device__ __forceinline__ void lerp_legacy(int o, int n_in, float scale, int& l
   l = fin - (float)lo;
 }
 
+// (cy, cx): the output is the H x W window at that offset of the image resized to the size
+// `sy` / `sx` were computed for (the aspect-preserving resize + random crop of
+// resize_images_and_labels, input_pipelines/utils.py:206-232); (0, 0) with the full size is
+// the plain resize
 __global__ __launch_bounds__(IN_THREADS) void prepare_images_kernel(
     const uint8_t* __restrict__ raw, int n, int Hr, int Wr, int H, int W, float sy, float sx,
-    float* __restrict__ out) {
+    int cy, int cx, float* __restrict__ out) {
   const long total = (long)n * H * W;
   const float inv255 = (float)(1.0 / 255.0);   // convert_image_dtype: cast * (1 / max)
   for (long id = (long)blockIdx.x * IN_THREADS + threadIdx.x; id < total;
@@ -33,8 +37,8 @@ __global__ __launch_bounds__(IN_THREADS) void prepare_images_kernel(
     const int b = (int)(id / ((long)W * H));
     int ylo, yhi, xlo, xhi;
     float yl, xl;
-    lerp_legacy(y, Hr, sy, ylo, yhi, yl);
-    lerp_legacy(x, Wr, sx, xlo, xhi, xl);
+    lerp_legacy(y + cy, Hr, sy, ylo, yhi, yl);
+    lerp_legacy(x + cx, Wr, sx, xlo, xhi, xl);
     const uint8_t* img = raw + (size_t)b * Hr * Wr * 3;
     const uint8_t* tl = img + ((size_t)ylo * Wr + xlo) * 3;
     const uint8_t* tr = img + ((size_t)ylo * Wr + xhi) * 3;
@@ -72,14 +76,14 @@ __global__ __launch_bounds__(IN_THREADS) void prepare_labels_kernel(
 
 }  // namespace
 
-hipError_t launch_prepare_images(const uint8_t* raw, int n, int Hr, int Wr, int H, int W,
-                                 float* out, hipStream_t s) {
+hipError_t launch_prepare_images(const uint8_t* raw, int n, int Hr, int Wr, int Hs, int Ws,
+                                 int cy, int cx, int H, int W, float* out, hipStream_t s) {
   const long total = (long)n * H * W;
   if (total <= 0) return hipSuccess;
   const long g = std::min<long>(ceil_div(total, IN_THREADS), 16384);
-  const float sy = (float)Hr / (float)H, sx = (float)Wr / (float)W;   // host IEEE division
+  const float sy = (float)Hr / (float)Hs, sx = (float)Wr / (float)Ws;   // host IEEE division
   hipLaunchKernelGGL(prepare_images_kernel, dim3((unsigned)g), dim3(IN_THREADS), 0, s, raw, n, Hr,
-                     Wr, H, W, sy, sx, out);
+                     Wr, H, W, sy, sx, cy, cx, out);
   return hipGetLastError();
 }
 

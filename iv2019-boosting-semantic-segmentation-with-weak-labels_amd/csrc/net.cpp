@@ -1926,8 +1926,20 @@ int seg_prepare_images(const uint8_t* raw, int n, int src_h, int src_w, int H, i
                        void* stream) {
   if (n < 0 || src_h <= 0 || src_w <= 0 || H <= 0 || W <= 0 || (n > 0 && (!raw || !out)))
     return set_err(nullptr, -EINVAL, "seg_prepare_images: bad arguments");
-  hipError_t e = launch_prepare_images(raw, n, src_h, src_w, H, W, out, (hipStream_t)stream);
+  hipError_t e = launch_prepare_images(raw, n, src_h, src_w, H, W, 0, 0, H, W, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_prepare_images");
+}
+
+int seg_prepare_images_crop(const uint8_t* raw, int n, int src_h, int src_w, int resized_h,
+                            int resized_w, int crop_y, int crop_x, int H, int W, float* out,
+                            void* stream) {
+  if (n < 0 || src_h <= 0 || src_w <= 0 || H <= 0 || W <= 0 || (n > 0 && (!raw || !out)) ||
+      crop_y < 0 || crop_x < 0 || crop_y + H > resized_h || crop_x + W > resized_w)
+    return set_err(nullptr, -EINVAL, "seg_prepare_images_crop: bad arguments (window %d,%d + %dx%d "
+                   "outside the resized %dx%d)", crop_y, crop_x, H, W, resized_h, resized_w);
+  hipError_t e = launch_prepare_images(raw, n, src_h, src_w, resized_h, resized_w, crop_y, crop_x,
+                                       H, W, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_prepare_images_crop");
 }
 
 int seg_prepare_labels(const uint8_t* raw, int n, int src_h, int src_w, int H, int W,

@@ -152,6 +152,21 @@ def prepare_images(raw, H: int, W: int, stream=None):
     return out
 
 
+def prepare_images_crop(raw, resized, offset, H: int, W: int, stream=None):
+    """raw: device uint8 [n, h, w, 3] -> bilinear resize to `resized` (h, w) -> the H x W window
+    at `offset` (y, x) -> fp32 [n, H, W, 3] in [-1, 1) (the aspect-preserving resize + random
+    crop of the weak-label streams, input_pipelines/utils.py:181-241)."""
+    import torch
+    from seg_hip import LIB, _ptr, _stream, check
+    assert raw.dtype == torch.uint8 and raw.dim() == 4 and raw.shape[-1] == 3 and raw.is_cuda
+    raw = raw.contiguous()
+    out = torch.empty((raw.shape[0], H, W, 3), dtype=torch.float32, device=raw.device)
+    check(LIB.seg_prepare_images_crop(_ptr(raw), raw.shape[0], raw.shape[1], raw.shape[2],
+                                      int(resized[0]), int(resized[1]), int(offset[0]),
+                                      int(offset[1]), H, W, _ptr(out), _stream(stream)))
+    return out
+
+
 def prepare_labels(raw, H: int, W: int, lids2cids, stream=None):
     """raw: device uint8 label ids [n, h, w] -> int32 prolabels [n, H, W] in training cids."""
     import ctypes

@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = [
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
     "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict", "seg_full_predictions",
     "seg_set_nesterov", "seg_set_defer_stem",
-    "seg_crc32c", "seg_prepare_images", "seg_prepare_labels",
+    "seg_crc32c", "seg_prepare_images", "seg_prepare_labels", "seg_prepare_images_crop",
 ]
 
 # int (*seg_allreduce_fn)(void* user, float* buf, int64_t n, void* stream)
@@ -112,6 +112,7 @@ def _load():
         "seg_tag_labels": (ip, [vp, ip, ip, ip, vp, vp]),
         "seg_set_bn_inference": (ip, [vp, ip]),
         "seg_prepare_images": (ip, [vp, ip, ip, ip, ip, ip, vp, vp]),
+        "seg_prepare_images_crop": (ip, [vp, ip, ip, ip, ip, ip, ip, ip, ip, ip, vp, vp]),
         "seg_prepare_labels": (ip, [vp, ip, ip, ip, ip, ip, ctypes.POINTER(ctypes.c_int32), ip,
                                     vp, vp]),
         "seg_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, vp, ctypes.c_size_t]),

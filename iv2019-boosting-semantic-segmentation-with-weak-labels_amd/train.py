@@ -1,9 +1,15 @@
 """Training entry point, drop-in for the reference's code/train.py.
 
 Same command line: ``python train.py <log_dir> {cityscapes,vistas} [flags]`` (plus the model
-flags of add_model_arguments and ``--psp_module``). The reference's TFRecord/OpenImages
-readers are out of scope (no datasets here): the train input_fn yields seeded synthetic
-batches in the reference's input contract (per_pixel_per_bbox_per_image.py:50-77).
+flags of add_model_arguments and ``--psp_module``). The reference hard-codes its dataset paths
+(train.py:17-20, 55-66 and the OpenImages modules); here they are flags:
+``--tfrecords_path_per_pixel`` (cityscapes / vistas TFRecords), ``--bboxes_index_path`` +
+``--bboxes_images_dir`` and ``--image_labels_index_path`` + ``--image_labels_images_dir``
+(OpenImages weak streams, JSON indices: input_pipelines/train_inputs.py). With a per-pixel
+TFRecord path the real-data input runs (host decode, device preprocessing and device bbox
+rasterisation, input_pipelines/train_inputs.heterogeneous_train_input); without one, the
+train input_fn yields seeded synthetic batches in the same input contract
+(per_pixel_per_bbox_per_image.py:50-77).
 Multi-GPU: ``torchrun --nproc-per-node N train.py ... --distribute`` (one process per GPU).
 """
 import os
@@ -45,6 +51,22 @@ def add_train_input_pipeline_arguments(argparser):
     argparser.add_argument('--Nb_per_bbox', type=int, default=8)
     argparser.add_argument('--Nb_per_image', type=int, default=4)
     argparser.add_argument('--max_steps', type=int, default=None)
+    # dataset locations (hard-coded constants in the reference)
+    argparser.add_argument('--tfrecords_path_per_pixel', type=str, nargs='*', default=None)
+    argparser.add_argument('--bboxes_index_path', type=str, default=None)
+    argparser.add_argument('--bboxes_images_dir', type=str, default=None)
+    argparser.add_argument('--image_labels_index_path', type=str, default=None)
+    argparser.add_argument('--image_labels_images_dir', type=str, default=None)
+    argparser.add_argument('--input_seed', type=int, default=0,
+                           help='seed of the shuffles and crop offsets (the reference seeds nothing)')
+
+
+def train_input_fn(settings):
+    """The real-data input when a per-pixel TFRecord path is given, else the synthetic one."""
+    if settings.tfrecords_path_per_pixel:
+        from input_pipelines.train_inputs import heterogeneous_train_input
+        return heterogeneous_train_input
+    return synthetic_train_input
 
 
 def _add_extra_args(settings):
@@ -69,7 +91,7 @@ def main(argv):
     add_model_arguments(ssargs.argparser)
     settings = ssargs.parse_args(argv)
     _add_extra_args(settings)
-    system = SemanticSegmentation({'train': synthetic_train_input}, model_fn, settings)
+    system = SemanticSegmentation({'train': train_input_fn(settings)}, model_fn, settings)
     return system.train(max_steps=settings.max_steps)
 
 

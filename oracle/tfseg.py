@@ -298,14 +298,17 @@ def nearest_ac_index(n_in: int, n_out: int):
     return torch.as_tensor(np.minimum(r.astype(np.int64), n_in - 1))
 
 
-def prepare_images_np(raw_u8, H: int, W: int):
+def prepare_images_np(raw_u8, H: int, W: int, resized=None, offset=(0, 0)):
     """Eval/train image preprocessing (input_cityscapes.py:190-209, 66-96):
     tf.image.convert_image_dtype (uint8 -> x * float32(1/255)), ResizeBilinear with
     align_corners=False (TF 1.12 legacy scaler: scale = in/out, in_f = o*scale, lo = (int),
     hi = min(lo+1, in-1), lerp = in_f - lo, all float32), from_0_1_to_m1_1 ((x-0.5)/0.5).
-    raw_u8 [n, h, w, 3] -> float32 [n, H, W, 3]."""
+    raw_u8 [n, h, w, 3] -> float32 [n, H, W, 3]. With `resized` (h', w') and `offset` (y, x):
+    the resize goes to h' x w' and the H x W window at the offset is returned (the
+    preserve_aspect_ratio resize + random crop, input_pipelines/utils.py:206-232)."""
     raw = np.asarray(raw_u8)
     x = raw.astype(np.float32) * np.float32(1.0 / 255.0)
+    rh, rw = resized if resized is not None else (H, W)
 
     def tables(n_in, n_out):
         scale = np.float32(np.float32(n_in) / np.float32(n_out))
@@ -313,8 +316,9 @@ def prepare_images_np(raw_u8, H: int, W: int):
         lo = fin.astype(np.int64)
         hi = np.minimum(lo + 1, n_in - 1)
         return lo, hi, (fin - lo.astype(np.float32)).astype(np.float32)
-    yl, yh, ylr = tables(raw.shape[1], H)
-    xl, xh, xlr = tables(raw.shape[2], W)
+    cy, cx = offset
+    yl, yh, ylr = (t[cy:cy + H] for t in tables(raw.shape[1], rh))
+    xl, xh, xlr = (t[cx:cx + W] for t in tables(raw.shape[2], rw))
     xlr = xlr[None, None, :, None]
     ylr = ylr[None, :, None, None]
     tl, tr = x[:, yl][:, :, xl], x[:, yl][:, :, xh]

@@ -26,6 +26,29 @@ def test_prepare_images_and_labels(cuda, src, dst):
     np.testing.assert_array_equal(la, prepare_labels_np(lab, *dst, L2C))
 
 
+@pytest.mark.parametrize("src,dst", [((80, 120), (64, 128)), ((100, 100), (64, 128)),
+                                     ((70, 150), (64, 128)), ((768, 1024), (512, 1024))])
+def test_prepare_images_crop(cuda, src, dst):
+    """Aspect-preserving resize (mode 'max') + crop window of the weak streams, bit-exact vs
+    resizing and slicing on the host (input_pipelines/utils.py:181-241), at several offsets
+    including both extremes."""
+    from input_pipelines.tfrecords import prepare_images_crop
+    from input_pipelines.weak_labels import aspect_preserving_size
+    from oracle.tfseg import prepare_images_np
+    rng = np.random.default_rng(sum(src))
+    raw = rng.integers(0, 256, (1,) + src + (3,), dtype=np.uint8)
+    rs = aspect_preserving_size(src[0], src[1], *dst)
+    full = prepare_images_np(raw, *rs)
+    for off in [(0, 0), (rs[0] - dst[0], rs[1] - dst[1]),
+                (int(rng.integers(0, rs[0] - dst[0] + 1)), int(rng.integers(0, rs[1] - dst[1] + 1)))]:
+        got = prepare_images_crop(torch.from_numpy(raw).to(cuda), rs, off, *dst).cpu().numpy()
+        ref = prepare_images_np(raw, *dst, resized=rs, offset=off)
+        np.testing.assert_array_equal(ref, full[:, off[0]:off[0] + dst[0], off[1]:off[1] + dst[1]])
+        np.testing.assert_array_equal(got, ref)
+    with pytest.raises(RuntimeError, match="outside"):
+        prepare_images_crop(torch.from_numpy(raw).to(cuda), rs, (rs[0] - dst[0] + 1, 0), *dst)
+
+
 def test_prepare_labels_out_of_table_ids(cuda):
     from input_pipelines.tfrecords import prepare_labels
     lab = torch.tensor([[[0, 40], [33, 255]]], dtype=torch.uint8, device=cuda)

@@ -153,3 +153,108 @@ def test_train_resumes_from_checkpoint(cuda, tmp_path):
         got = ctx.named(b)
         assert all(np.array_equal(got[k], ref[k]) for k in ref), b
     mh.release_contexts()
+
+
+def test_train_main_real_data_matches_oracle(cuda, tmp_path, capsys, monkeypatch):
+    """``train.main`` on the committed tiny real-data set
+    (tests/golden/tiny_train: a per-pixel TFRecord + OpenImages-style box / tag indices and
+    JPEGs) trains 2 steps through host decode -> device preprocessing (seg_prepare_images /
+    _labels / _images_crop) -> device bbox rasterisation; every batch it consumed is captured
+    and the oracle's own 2-step chain on those decoded batches (weak maps restated on the host
+    by weak_labels.bbox_label_map / generate_tag_rla) matches the logged losses and the
+    parameter / momentum / EMA changes, with the tolerances of the synthetic test above.
+    The device image crop path is pinned bit-exactly to oracle.prepare_images_np on the first
+    bbox image of each batch."""
+    import json
+    import os
+    import train
+    from estimator.define_estimator_hierarchical import get_or_create_global_step
+    from input_pipelines import train_inputs
+    from input_pipelines.weak_labels import bbox_label_map, generate_tag_rla
+    from models import resnet50_extended_model_hierarchical as mh
+    from oracle.tfseg import prepare_images_np
+    tiny = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tiny_train")
+    mh.release_contexts()
+    get_or_create_global_step().value = 0
+    H, W = 64, 128
+    captured, crops = [], []
+    orig = train_inputs.heterogeneous_train_input
+    orig_crop = train_inputs.OpenImagesStream.take
+
+    def take(self, n):   # record the decoded weak images (to pin the device crop path)
+        out = orig_crop(self, n)
+        crops.append([o[1] for o in out])
+        return out
+
+    def capture(config, params):
+        for feats, labels in orig(config, params):
+            captured.append((feats["proimages"].cpu().numpy().copy(),
+                             labels["prolabels_per_pixel"].cpu().numpy().copy(),
+                             list(labels["prolabels_per_bbox"]), list(labels["prolabels_per_image"])))
+            yield feats, labels
+    monkeypatch.setattr(train_inputs, "heterogeneous_train_input", capture)
+    monkeypatch.setattr(train_inputs.OpenImagesStream, "take", take)
+    argv = [str(tmp_path / "logs"), "cityscapes", "--max_steps", "2", "--compute_dtype", "fp32",
+            "--height_feature_extractor", str(H), "--width_feature_extractor", str(W),
+            "--Nb_per_pixel", "2", "--Nb_per_bbox", "1", "--Nb_per_image", "1",
+            "--learning_rate_initial", "1e-5", "--save_summaries_steps", "1",
+            "--save_checkpoints_steps", "100",
+            "--tfrecords_path_per_pixel", os.path.join(tiny, "cityscapes.tfrecord"),
+            "--bboxes_index_path", os.path.join(tiny, "bboxes.json"),
+            "--bboxes_images_dir", os.path.join(tiny, "images"),
+            "--image_labels_index_path", os.path.join(tiny, "tags.json"),
+            "--image_labels_images_dir", os.path.join(tiny, "images")]
+    assert train.main(argv) == 2
+    out = capsys.readouterr().out
+    logged = [tuple(float(v) for v in m) for m in
+              re.findall(r"step \d+: total ([-\d.]+) l1 ([-\d.]+) l2v ([-\d.]+) l2h ([-\d.]+)", out)]
+    assert len(logged) == 2 and len(captured) >= 2, out
+    ctx = next(iter(mh._CONTEXTS.values()))
+    # the per-pixel labels are training cids (void = 19) and the crop path is bit-exact
+    for k in range(2):
+        _, px, boxes, _ = captured[k]
+        assert px.min() >= 0 and px.max() <= 19
+        cids, coords, src, rs, off = boxes[0]
+        ref = prepare_images_np(crops[2 * k][0][None], H, W, resized=rs, offset=off)[0]
+        assert np.array_equal(captured[k][0][2], ref)
+    cfg = SegConfig(height=H, width=W, nb_pp=2, nb_pb=1, nb_pi=1, pyramid="none")
+    p0 = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=0).items()}
+
+    def chain(dtype):
+        params = {k: v.astype(np.float64) for k, v in p0.items()}
+        mom = ema = None
+        losses = []
+        for k in range(2):
+            im, px, boxes, tags = captured[k]
+            bb = np.stack([bbox_label_map(c, co, s, r, o, (H, W)) for c, co, s, r, o in boxes])
+            tg = np.stack([np.broadcast_to(generate_tag_rla(list(t)), (H, W, 15)) for t in tags])
+            net = OracleNet(cfg, params, dtype=dtype)
+            L, _, _, new_p, mom, ema, _ = net.train_step(im, px, bb.astype(np.float32),
+                                                         tg.astype(np.float32), lr=1e-5,
+                                                         mom_state=mom, ema_state=ema,
+                                                         ema_decay=0.9, step=k)
+            losses.append(tuple(float(L[n].detach()) for n in (
+                "total", "l1_segmentation", "l2_vehicle_segmentation", "l2_human_segmentation")))
+            params = {n: v.detach().numpy() for n, v in new_p.items()}
+        return losses, params, {n: v.numpy() for n, v in mom.items()}, \
+            {n: v.detach().numpy() for n, v in ema.items()}
+
+    ref_losses, ref_p, ref_m, ref_e = chain(torch.float64)
+    l32, p32, m32, e32 = chain(torch.float32)
+    rtol = np.array([1e-3, 1e-3, 3e-2, 3e-2])
+    for k, (got, ref) in enumerate(zip(logged, ref_losses)):
+        got, ref = np.array(got), np.array(ref)
+        assert np.all(np.abs(got - ref) <= rtol * np.abs(ref) + 5e-4), (k, got, ref, l32[k])
+    nat_p, nat_m, nat_e = ctx.named("params"), ctx.named("momentum"), ctx.named("ema")
+    keys = list(ref_m)
+    flat = lambda d, ks: np.concatenate([np.asarray(d[k], np.float64).reshape(-1) for k in ks])
+    w0 = flat(p0, keys)
+    rows = []
+    for what, nat, ref, r32, base in (("momentum", nat_m, ref_m, m32, 0), ("w2 - w0", nat_p, ref_p, p32, w0),
+                                      ("ema - w0", nat_e, ref_e, e32, w0)):
+        gap = _rel(flat(r32, keys) - base, flat(ref, keys) - base)
+        err = _rel(flat(nat, keys) - base, flat(ref, keys) - base)
+        rows.append((what, err, gap))
+    assert all(err < max(1e-2, 3 * gap) for _, err, gap in rows), rows
+    assert json.load(open(os.path.join(tiny, "tags.json")))
+    mh.release_contexts()
