@@ -7,7 +7,7 @@ out=$1; shift
 mkdir -p $out
 export TMPDIR=/tmp
 for v in default "$@"; do
-  if [ "$v" = default ]; then unset SEG_HIP_LIB; else export SEG_HIP_LIB=$PWD/iv2019-boosting-semantic-segmentation-with-weak-labels_amd/build/$v/libseg_hip.so; fi
+  if [ "$v" = default ]; then unset SEG_HIP_LIB; else export SEG_HIP_LIB=$PWD/ab/$v/libseg_hip.so; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/$v -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-eval --no-profile > $out/$v.log 2>&1
   python3 tools/rocpd_stats.py $out/$v/run_results.db $out/$v.csv > $out/$v.txt
   python3 tools/timeline.py $out/$v/run_results.db > $out/$v.timeline.txt || true
