@@ -640,7 +640,14 @@ constexpr int WPP_LDS = 2 * WBUF;
 
 __device__ __forceinline__ int wpp_swz(int row, int ch) { return ch ^ (2 * (row & 3) + 8 * ((row >> 3) & 1)); }
 
-template <typename E, int FAST>   // FAST: Wo >= 64 (a K-tile's rows need at most one row carry)
+// FAST: 1 = Wo >= 64 (a K-tile's rows need at most one row carry); 2 = strip order (Wo a
+// multiple of 64): a K-tile is 64 pixels of one output row, and consecutive K-tiles walk DOWN a
+// 64-pixel-wide column strip (n, strip, ho; ho fastest) instead of along the rows. A dilated 3x3
+// layer reads input rows ho - d, ho, ho + d for output row ho, so one input row is re-read d
+// K-tiles later in strip order against d * Wo / 64 K-tiles in raster order: with the 32
+// workgroups of an XCD walking the same split, the reuse window is ~1 MB of L2 instead of ~4 MB
+// (block4, rate 4, Wo 256), which is the XCD's whole L2.
+template <typename E, int FAST>
 __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
   typedef typename Half<E>::V V;
   constexpr int BM = 256, BN = 256, PK = 64;
@@ -660,10 +667,12 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
   const int rem = wg - split * mtn * ntn;
   const int nt_ = rem / mtn, mt_ = rem - nt_ * mtn;
   const int m0 = mt_ * BM, n0 = nt_ * BN;
+  // splits cut the K-tile sequence (strip order: whole K-tiles of 64 pixels; raster: pixels)
   const int chunk = ((P + a.splits - 1) / a.splits + PK - 1) / PK * PK;
   const int p_begin = split * chunk;
   const int p_end = (p_begin + chunk < P) ? p_begin + chunk : P;
   const int nk = p_end > p_begin ? (p_end - p_begin + PK - 1) / PK : 0;
+  const int nstrips = a.Wo / PK;
 
   const auto rs_dy = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, (int)((long)P * a.lddy * 2), 0x00020000);
   const auto rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0,
@@ -692,9 +701,17 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
     b_toff[j] = (b_dh[j] * a.W + b_dw[j]) * a.ldx + ci;
   }
 
-  // next K-tile to issue: first pixel p0 decoded to (n, ho, wo), stepped by PK pixels
+  // next K-tile to issue: first pixel p0 decoded to (n, ho, wo), stepped by PK pixels (raster)
+  // or by one row down the strip (strip order: K-tile index t = (n * nstrips + strip) * Ho + ho)
   int nx_p0 = p_begin, nx_n, nx_ho, nx_wo;
-  {
+  if constexpr (FAST == 2) {
+    const int t = p_begin / PK;
+    nx_ho = t % a.Ho;
+    const int u = t / a.Ho;
+    nx_wo = (u % nstrips) * PK;
+    nx_n = u / nstrips;
+    nx_p0 = (nx_n * a.Ho + nx_ho) * a.Wo + nx_wo;
+  } else {
     nx_wo = p_begin % a.Wo;
     const int t = p_begin / a.Wo;
     nx_ho = t % a.Ho;
@@ -704,13 +721,22 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
   int hb[2], wb[2], pixb[2];
   bool pv[2];
   int cur_p0 = 0, cur_prem = 0;
+  int kt_left = nk;   // strip order: K-tiles left in this split (all full)
   auto decode_next = [&]() {
     cur_p0 = nx_p0;
-    cur_prem = p_end - nx_p0;
+    if constexpr (FAST == 2) {
+      cur_prem = kt_left-- > 0 ? PK : 0;
+    } else {
+      cur_prem = p_end - nx_p0;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       int n, ho, wo;
-      if constexpr (FAST) {
+      if constexpr (FAST == 2) {
+        wo = nx_wo + r_[i];
+        ho = nx_ho;
+        n = nx_n;
+      } else if constexpr (FAST) {
         wo = nx_wo + r_[i];
         const bool c = wo >= a.Wo;
         wo = c ? wo - a.Wo : wo;
@@ -730,11 +756,20 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       pixb[i] = ((n * a.H + hb[i]) * a.W + wb[i]) * a.ldx;
       pv[i] = r_[i] < cur_prem;
     }
-    nx_p0 += PK;
-    nx_wo += PK;
-    while (nx_wo >= a.Wo) {
-      nx_wo -= a.Wo;
-      if (++nx_ho == a.Ho) { nx_ho = 0; ++nx_n; }
+    if constexpr (FAST == 2) {
+      if (++nx_ho == a.Ho) {
+        nx_ho = 0;
+        nx_wo += PK;
+        if (nx_wo == a.Wo) { nx_wo = 0; ++nx_n; }
+      }
+      nx_p0 = (nx_n * a.Ho + nx_ho) * a.Wo + nx_wo;
+    } else {
+      nx_p0 += PK;
+      nx_wo += PK;
+      while (nx_wo >= a.Wo) {
+        nx_wo -= a.Wo;
+        if (++nx_ho == a.Ho) { nx_ho = 0; ++nx_n; }
+      }
     }
   };
 
@@ -746,14 +781,28 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       auto* ldst = (__attribute__((address_space(3))) void*)(dst + (i * 8 + wave) * 1024);
       if (hid < 2) {
         const int j = hid * 2 + i;
-        const uint32_t off = r_[i] < cur_prem ? a_voff[j] + (uint32_t)(cur_p0 * a.lddy * 2) : OOB;
+        uint32_t off = r_[i] < cur_prem ? a_voff[j] + (uint32_t)(cur_p0 * a.lddy * 2) : OOB;
+#ifdef WG_DBG_SAMELINE   // A/B diagnostics only (wrong results): every row reads the tile's row 0
+        off = a_voff[j] - (uint32_t)(r_[i] * a.lddy * 2);
+#endif
+#ifndef WG_DBG_NODMA
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_dy, ldst, 16, off, 0, 0, 0);
+#else
+        (void)off; (void)ldst;
+#endif
       } else {
         const int j = (hid - 2) * 2 + i;
         const int hi = hb[i] + b_dh[j], wi = wb[i] + b_dw[j];
         const bool ok = pv[i] & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
-        const uint32_t off = ok ? (uint32_t)((pixb[i] + b_toff[j]) * 2) : OOB;
+        uint32_t off = ok ? (uint32_t)((pixb[i] + b_toff[j]) * 2) : OOB;
+#ifdef WG_DBG_SAMELINE
+        off = (uint32_t)(b_toff[j] > 0 ? b_toff[j] * 2 : 0);
+#endif
+#ifndef WG_DBG_NODMA
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, ldst, 16, off, 0, 0, 0);
+#else
+        (void)off; (void)ldst;
+#endif
       }
     }
   };
@@ -901,6 +950,12 @@ __global__ __launch_bounds__(PP_THREADS, 1) void conv_wgrad_pp_kernel(WgradArgs 
 
 }  // namespace
 
+// A/B switch read once per process (experiments only)
+static bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '1';
+}
+
 // 256 x 256 wgrad tiles with operands < 2^31 bytes (32-bit buffer offsets)
 bool conv_wgrad_pp_ok(const WgradArgs& a) {
   const long P = (long)a.N * a.Ho * a.Wo;
@@ -917,10 +972,15 @@ hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(PP_THREADS), WPP_LDS, s, a);
     return hipGetLastError();
   };
+  // strip order where the rows split into whole 64-pixel K-tiles and the pixel rows repeat
+  // across taps (KH > 1); 1x1 layers read every x row once, raster order is as good there
+  const bool strip = (a.Wo % 64) == 0 && a.KH > 1 && !getenv_flag("SEG_WGRAD_RASTER");
   if (dtype == SEG_F16) {
+    if (strip) return launch(conv_wgrad_pp_kernel<f16_t, 2>);
     if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<f16_t, 1>);
     return launch(conv_wgrad_pp_kernel<f16_t, 0>);
   }
+  if (strip) return launch(conv_wgrad_pp_kernel<bf16_t, 2>);
   if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<bf16_t, 1>);
   return launch(conv_wgrad_pp_kernel<bf16_t, 0>);
 }
