@@ -37,6 +37,19 @@ __device__ unsigned long long g_pp_dbg[256 * 16 * 4];
 #define PP_TS(it, k)
 #endif
 
+#ifdef WG_DBG_TIMING
+// A/B only: per-wave segment timestamps (s_memtime) of the wgrad ping-pong loop, blocks 0-7,
+// K-tiles 16-23, 8 stamps per K-tile (loop top, before / after barrier A, after the first MFMA
+// segment, after barrier B, before / after barrier C, after the second MFMA segment)
+__device__ unsigned long long g_wg_dbg[8 * 8 * 8 * 8];
+#define WG_TS(kb, k)                                                                           \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 8 && (kb) >= 16 && (kb) < 24)                     \
+    g_wg_dbg[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + ((kb) - 16)) * 8 + (k)] =             \
+        __builtin_amdgcn_s_memtime()
+#else
+#define WG_TS(kb, k)
+#endif
+
 namespace {
 
 constexpr int PP_THREADS = 512;
@@ -631,6 +644,10 @@ hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s) {
 // Operands come through buffer resources: dy rows are one add per DMA, x rows are decoded once
 // per K-tile and lane (pixel -> n, ho, wo by row carries) and shared by both x halves.
 // Split-K over pixels into fp32 slabs as in v2 (reduced by splitk_reduce).
+// Round 3: the 8 DMA pieces of a K-tile are split 4 / 4 over the two load segments (it was 6 / 2:
+// per-segment s_memtime stamps, tools/wg_timing.py, showed the phase-0 load segment at ~1300
+// cycles against ~650 for the partner's MFMA segment, each LDS-DMA piece costing ~150 cycles);
+// block4 3x3 622 -> 599 us, the 1x1 layers 2-6 % (profiles/r03_wgrad_bal.txt).
 // ======================================================================================
 namespace {
 
@@ -873,52 +890,77 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
           acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfq[qn][j][s], acc[qm][qn][i][j]);
   };
   if (nk > 0) {
+    // balanced DMA: 4 of the 8 DMA pieces per K-tile in each load segment. K-tile k's halves
+    // are issued A0 + B1 in L1(k-2) and B0 + A1 in L0(k-1) (x rows decoded once, at the first
+    // pair). Every load segment ends with its fragment reads complete (lgkmcnt(0)), so a DMA
+    // issued after the next barrier cannot overwrite a half another wave is still reading.
     decode_next();
     issue_half(0, 0);
-    issue_half(0, 2);
     issue_half(0, 3);
+    issue_half(0, 2);
     issue_half(0, 1);
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // halves 0, 2, 3 landed (1 in flight)
+    if (nk > 1) {
+      decode_next();
+      issue_half(1, 0);
+      issue_half(1, 3);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // A0, B1, B0 of K-tile 0 landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
     pp_barrier();
     if (wm == 1) pp_barrier();
-    // static priority for the second-dispatched wave row (waves 4-7, the arbitration loser);
-    // per-segment priority flips measured 2-5 % slower on the wgrad 1x1 layers
     if (wm == 1) __builtin_amdgcn_s_setprio(1);
-    {
-      // two phases per K-tile as the NT kernel: (0,0), (0,1) from dy co 0-127 and both x
-      // halves, refilling those three of kb+1; then (1,1), (1,0) from dy co 128-255
-      for (int kb = 0; kb < nk; ++kb) {
-        const bool more = kb + 1 < nk;
-        if (more) decode_next();
-        read_a(kb, 0);
-        read_b(kb, 0);
-        read_b(kb, 1);
-        if (more) {
-          issue_half(kb + 1, 0);
-          issue_half(kb + 1, 2);
-          issue_half(kb + 1, 3);
-        }
-        if (wm == 1) {
-          if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        pp_barrier();
-        mfma_q(0, 0);
-        mfma_q(0, 1);
-        if (wm == 0) {
-          if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        pp_barrier();
-        read_a(kb, 1);
-        if (more) issue_half(kb + 1, 1);
-        if (more && wm == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        pp_barrier();
-        mfma_q(1, 1);
-        mfma_q(1, 0);
-        if (more && wm == 0) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        pp_barrier();
+    for (int kb = 0; kb < nk; ++kb) {
+      const bool m1 = kb + 1 < nk, m2 = kb + 2 < nk;
+      WG_TS(kb, 0);
+      read_a(kb, 0);
+      read_b(kb, 0);
+      read_b(kb, 1);
+      if (m1) {
+        issue_half(kb + 1, 2);
+        issue_half(kb + 1, 1);
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // L1(kb) reads A1(kb): everything after it may stay in flight (A0, B1, B0, A1 of kb+1)
+      if (wm == 1) {
+        if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      WG_TS(kb, 1);
+      pp_barrier();
+      WG_TS(kb, 2);
+      mfma_q(0, 0);
+      mfma_q(0, 1);
+      WG_TS(kb, 3);
+      if (wm == 0) {
+        if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pp_barrier();
+      WG_TS(kb, 4);
+      read_a(kb, 1);
+      if (m2) {
+        decode_next();
+        issue_half(kb + 2, 0);
+        issue_half(kb + 2, 3);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // L0(kb+1) reads A0, B0, B1 of kb+1: A1(kb+1), A0(kb+2), B1(kb+2) may stay in flight
+      if (wm == 1 && m1) {
+        if (m2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      WG_TS(kb, 5);
+      pp_barrier();
+      WG_TS(kb, 6);
+      mfma_q(1, 1);
+      mfma_q(1, 0);
+      WG_TS(kb, 7);
+      if (wm == 0 && m1) {
+        if (m2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      pp_barrier();
     }
     if (wm == 0) pp_barrier();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -984,6 +1026,12 @@ hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s) {
   if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<bf16_t, 1>);
   return launch(conv_wgrad_pp_kernel<bf16_t, 0>);
 }
+
+#ifdef WG_DBG_TIMING
+extern "C" int seg_dbg_wg_timing(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_dbg), sizeof(g_wg_dbg)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef PP_DBG_TIMING
 extern "C" int seg_dbg_pp_timing(void* host) {
