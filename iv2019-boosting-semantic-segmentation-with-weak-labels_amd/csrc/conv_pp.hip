@@ -255,6 +255,28 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   f32x4_t acc[2][2][4][2];   // [qm][qn][fi][fj]
 
   V af[4][2], bfq[2][2][2];   // [frag][k-half]; B per quadrant qn: B0 kept for phase 3
+#ifdef NT_DBG_AFOLD
+  // A/B diagnostic only (wrong results): the cost of folding the producer's BN apply + ReLU
+  // into this conv's A operand in registers (per-lane scale / shift of its 8 channels)
+  float fs[8], fb[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) { fs[c] = 1.f + 1e-3f * (float)(lane + c); fb[c] = -1e-3f * (float)(c + lq); }
+  auto fold = [&](V& f) {
+    uint32_t w[4];
+    __builtin_memcpy(w, &f, 16);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const float lo = fmaxf(fmaf(__uint_as_float(w[h] << 16), fs[2 * h], fb[2 * h]), 0.f);
+      const float hi = fmaxf(fmaf(__uint_as_float(w[h] & 0xffff0000u), fs[2 * h + 1], fb[2 * h + 1]), 0.f);
+      const E el = TypeOps<E>::from_f(lo), eh = TypeOps<E>::from_f(hi);
+      uint16_t bl, bh;
+      __builtin_memcpy(&bl, &el, 2);
+      __builtin_memcpy(&bh, &eh, 2);
+      w[h] = (uint32_t)bl | ((uint32_t)bh << 16);
+    }
+    __builtin_memcpy(&f, w, 16);
+  };
+#endif
   auto read_a = [&](const char* buf, int qm) {
     const char* A = buf + qm * HALF;
 #pragma unroll
@@ -263,6 +285,12 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) af[i][s] = *(const V*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
     }
+#ifdef NT_DBG_AFOLD
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fold(af[i][s]);
+#endif
   };
   auto read_b = [&](const char* buf, int qn) {
     const char* B = buf + (2 + qn) * HALF;
@@ -318,41 +346,59 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 
   {
     // two phases per K-tile (half the barriers): phase 0 = quadrants (0,0), (0,1) from A0, B0,
-    // B1, refilling A0, B0, B1 of kb+1 (all read in phase 0 of kb-1 by both wave rows); phase 1
-    // = (1,1), (1,0) from A1, refilling A1 of kb+1. Waits: before phase 1, A1(kb) with the 6
-    // DMAs of phase 0 still in flight; before phase 0 of kb+1, its A0, B0, B1 with A1(kb+1) in
-    // flight
+    // B1; phase 1 = (1,1), (1,0) from A1 (B kept in registers).
+    // balanced DMA (as the weight-gradient kernel): K-tile k's halves are issued A0 + B1 in
+    // L1(k-2) and B0 + A1 in L0(k-1) (K-tile 1's A0 + B1 in L0(0): buffer 1 holds the previous
+    // tile's epilogue staging until the tile-start barrier); every load segment ends with its
+    // LDS reads complete, so a DMA issued after the next barrier cannot overwrite a half that
+    // another wave is still reading
+    KT tn1{};
     for (int kb = 0; kb < nk; ++kb) {
       const char* buf = smem + (kb & 1) * BUF;
-      const bool more = kb + 1 < nk;
-      const KT tn = ktile_next();
+      const bool m1 = kb + 1 < nk, m2 = kb + 2 < nk;
       read_a(buf, 0);
       read_b(buf, 0);
       read_b(buf, 1);
-      if (more) {
-        issue_half(kb + 1, tn, 0);
-        issue_half(kb + 1, tn, 2);
-        issue_half(kb + 1, tn, 3);
+      if (kb == 0 && m1) {
+        tn1 = ktile_next();
+        issue_half(1, tn1, 0);
+        issue_half(1, tn1, 3);
       }
+      if (m1) {
+        issue_half(kb + 1, tn1, 2);
+        issue_half(kb + 1, tn1, 1);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (wm == 1) {
-        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       pp_barrier();
       mfma_q(0, 0);
       mfma_q(0, 1);
       if (wm == 0) {
-        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       pp_barrier();
       read_a(buf, 1);
-      if (more) issue_half(kb + 1, tn, 1);
-      if (more && wm == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if (m2) {
+        tn1 = ktile_next();
+        issue_half(kb + 2, tn1, 0);
+        issue_half(kb + 2, tn1, 3);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (m1 && wm == 1) {
+        if (m2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
       pp_barrier();
       mfma_q(1, 1);
       mfma_q(1, 0);
-      if (more && wm == 0) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if (m1 && wm == 0) {
+        if (m2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
       pp_barrier();
     }
   }
