@@ -220,10 +220,11 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   };
 
   // half ids: 0 = A0, 1 = A1, 2 = B0, 3 = B1 (LDS offset hid * HALF inside a K-tile buffer)
-  auto issue_half = [&](int kb, const KT& t, int hid) {
+  auto issue_half = [&](int kb, const KT& t, int hid, int i0 = 0, int i1 = 2) {
     char* dst = smem + (kb & 1) * BUF + hid * HALF;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (i < i0 || i >= i1) continue;
       auto* ldst = (__attribute__((address_space(3))) void*)(dst + (i * 8 + wave) * 1024);
       if (hid < 2) {
         const int j = hid * 2 + i;
@@ -690,10 +691,13 @@ hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s) {
 // Operands come through buffer resources: dy rows are one add per DMA, x rows are decoded once
 // per K-tile and lane (pixel -> n, ho, wo by row carries) and shared by both x halves.
 // Split-K over pixels into fp32 slabs as in v2 (reduced by splitk_reduce).
-// Round 3: the 8 DMA pieces of a K-tile are split 4 / 4 over the two load segments (it was 6 / 2:
-// per-segment s_memtime stamps, tools/wg_timing.py, showed the phase-0 load segment at ~1300
-// cycles against ~650 for the partner's MFMA segment, each LDS-DMA piece costing ~150 cycles);
-// block4 3x3 622 -> 599 us, the 1x1 layers 2-6 % (profiles/r03_wgrad_bal.txt).
+// Round 3: the 8 DMA pieces of a K-tile are spread so that the load segments (fragment reads)
+// and the MFMA segments of the partner wave row take about the same time: per-segment s_memtime
+// stamps (tools/wg_timing.py) had the load segments at 1.5-2x the MFMA segments. 6/2 -> 4/4 over
+// the two load segments (block4 3x3 622 -> 599 us), then the four dy pieces (one VALU of address
+// math each) moved into the MFMA segments, one per quadrant (599 -> 572 us; the 1x1 layers 2-6 %
+// each step; profiles/r03_wgrad_bal.txt, r03_wgrad_mseg.txt). Moving the x pieces too, or the
+// x-row decode, made the MFMA segments the longer ones (rejected).
 // ======================================================================================
 namespace {
 
@@ -837,10 +841,12 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
   };
 
   // half ids: 0 = dy co 0-127, 1 = dy co 128-255, 2 = x cols 0-127, 3 = x cols 128-255
-  auto issue_half = [&](int kb, int hid) {
+  // (pieces i0 .. i1-1 of the half: 2 DMA instructions per wave and half)
+  auto issue_half = [&](int kb, int hid, int i0 = 0, int i1 = 2) {
     char* dst = smem + (kb & 1) * WBUF + hid * WHALF;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (i < i0 || i >= i1) continue;
       auto* ldst = (__attribute__((address_space(3))) void*)(dst + (i * 8 + wave) * 1024);
       if (hid < 2) {
         const int j = hid * 2 + i;
@@ -924,22 +930,28 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) frag2(off + b_rb[j], bfq[qn][j][0], bfq[qn][j][1]);
   };
-  auto mfma_q = [&](int qm, int qn) {
+  // one quadrant's 16 MFMAs with one DMA piece of (kbi, hid) issued after the first 8
+  auto mfma_q_dma = [&](int qm, int qn, bool dma, int kbi, int hid, int piece) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm fragment reads
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s) {
+      if (s == 1 && dma) {
+        __builtin_amdgcn_sched_barrier(0);
+        issue_half(kbi, hid, piece, piece + 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[qm][qn][i][j] = Half<E>::mma(af[i][s], bfq[qn][j][s], acc[qm][qn][i][j]);
+    }
   };
   if (nk > 0) {
-    // balanced DMA: 4 of the 8 DMA pieces per K-tile in each load segment. K-tile k's halves
-    // are issued A0 + B1 in L1(k-2) and B0 + A1 in L0(k-1) (x rows decoded once, at the first
-    // pair). Every load segment ends with its fragment reads complete (lgkmcnt(0)), so a DMA
-    // issued after the next barrier cannot overwrite a half another wave is still reading.
+    // DMA in the MFMA segments: per K-tile, B0(kb+1) in L0(kb), A1(kb+1) in M0(kb) (one piece
+    // per quadrant), B1(kb+2) in L1(kb), A0(kb+2) in M1(kb). The dy pieces (one VALU of
+    // address math each) move out of the load segments, which were ~1.5x the MFMA segments.
     decode_next();
     issue_half(0, 0);
     issue_half(0, 3);
@@ -947,8 +959,8 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
     issue_half(0, 1);
     if (nk > 1) {
       decode_next();
-      issue_half(1, 0);
       issue_half(1, 3);
+      issue_half(1, 0);
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // A0, B1, B0 of K-tile 0 landed
     } else {
       asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -962,21 +974,18 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       read_a(kb, 0);
       read_b(kb, 0);
       read_b(kb, 1);
-      if (m1) {
-        issue_half(kb + 1, 2);
-        issue_half(kb + 1, 1);
-      }
+      if (m1) issue_half(kb + 1, 2);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // L1(kb) reads A1(kb): everything after it may stay in flight (A0, B1, B0, A1 of kb+1)
+      // A1(kb) (issued in M0(kb-1)) landed: younger are B1(kb+1), A0(kb+1), B0(kb+1) (+A1(kb+1))
       if (wm == 1) {
-        if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (m1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       WG_TS(kb, 1);
       pp_barrier();
       WG_TS(kb, 2);
-      mfma_q(0, 0);
-      mfma_q(0, 1);
+      mfma_q_dma(0, 0, m1, kb + 1, 1, 0);
+      mfma_q_dma(0, 1, m1, kb + 1, 1, 1);
       WG_TS(kb, 3);
       if (wm == 0) {
         if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -987,20 +996,19 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       read_a(kb, 1);
       if (m2) {
         decode_next();
-        issue_half(kb + 2, 0);
         issue_half(kb + 2, 3);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // L0(kb+1) reads A0, B0, B1 of kb+1: A1(kb+1), A0(kb+2), B1(kb+2) may stay in flight
+      // A0, B0, B1 of kb+1 landed: younger than B0(kb+1) are A1(kb+1), B1(kb+2) (+A0(kb+2))
       if (wm == 1 && m1) {
-        if (m2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (m2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       }
       WG_TS(kb, 5);
       pp_barrier();
       WG_TS(kb, 6);
-      mfma_q(1, 1);
-      mfma_q(1, 0);
+      mfma_q_dma(1, 1, m2, kb + 2, 0, 0);
+      mfma_q_dma(1, 0, m2, kb + 2, 0, 1);
       WG_TS(kb, 7);
       if (wm == 0 && m1) {
         if (m2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");

@@ -1,3 +1,6 @@
 set -e
-mkdir -p gpurun_out/s9
-OPS="fwd" LAYERS="b4c3 b3c3 b3c2 b4c2 b4c1" timeout -k 10 300 tools/ab_ops.sh afold > gpurun_out/s9/ab_afold.txt 2>&1
+out=gpurun_out/s7
+mkdir -p $out
+export TMPDIR=/tmp
+echo suite; timeout -k 10 1000 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $out/suite.txt 2>&1
+echo done
