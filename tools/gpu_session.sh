@@ -1,6 +1,12 @@
 set -e
-out=gpurun_out/s7
+out=gpurun_out/s9
 mkdir -p $out
 export TMPDIR=/tmp
-echo suite; timeout -k 10 1000 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $out/suite.txt 2>&1
+echo parity; SEG_CU_SPLIT=3 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_step.py tests/test_gpu_train.py > $out/parity.txt 2>&1
+echo ab
+for r in 1 2; do for v in 0 2 3 4 5; do
+  if [ $v = 0 ]; then unset SEG_CU_SPLIT; else export SEG_CU_SPLIT=$v; fi
+  timeout -k 10 200 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-eval > $out/b.log 2>&1
+  echo "split=$v $(tail -1 $out/b.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["value"])')"
+done; done > $out/ab.txt
 echo done
