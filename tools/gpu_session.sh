@@ -1,15 +1,12 @@
 set -e
-out=gpurun_out/s11
+out=gpurun_out/s12
 mkdir -p $out
 export TMPDIR=/tmp
-for v in default ru4 ru8 ru12; do
-  if [ "$v" = default ]; then unset SEG_HIP_LIB; else export SEG_HIP_LIB=$PWD/ab/$v/libseg_hip.so; fi
-  SEG_SIDE_STREAM=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/$v -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-eval --no-profile > $out/$v.log 2>&1
-  python3 tools/rocpd_stats.py $out/$v/run_results.db $out/$v.csv > $out/$v.txt
-  rm -rf $out/$v
-  echo "== $v"; grep -i "bn_bwd_reduce" $out/$v.txt
-done > $out/summary.txt
-unset SEG_HIP_LIB
-timeout -k 10 600 tools/ab_bench.sh ru8 ru12 > $out/ab.txt 2>&1
-SEG_HIP_LIB=$PWD/ab/ru8/libseg_hip.so timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_step.py > $out/parity.txt 2>&1
+echo parity; SEG_WGRAD_LATE=1 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_step.py tests/test_gpu_train.py tests/test_gpu_buckets.py > $out/parity.txt 2>&1
+echo ab
+for r in 1 2 3; do for v in 0 1; do
+  if [ $v = 0 ]; then unset SEG_WGRAD_LATE; else export SEG_WGRAD_LATE=1; fi
+  timeout -k 10 200 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-eval > $out/b.log 2>&1
+  echo "late=$v $(tail -1 $out/b.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["value"])')"
+done; done > $out/ab.txt
 echo done
