@@ -80,6 +80,11 @@ hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s);
 bool conv_wgrad_pp_ok(const WgradArgs& a);
 hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s);
 bool conv_wgrad_v2_ok(const WgradArgs& a);
+// small-channel 3 x 3 stride-1 weight gradient on input patches (wgrad_patch.hip): Co, C in
+// {64, 128}, Wo % 64 == 0; grid = conv_wgrad_patch_blocks x splits
+bool conv_wgrad_patch_ok(const WgradArgs& a);
+int conv_wgrad_patch_blocks(const WgradArgs& a);
+hipError_t launch_conv_wgrad_patch(int dtype, const WgradArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad_v2(int dtype, const WgradArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad_v2_tile(int dtype, const WgradArgs& a, int bm, int bn, hipStream_t s);
 void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn);

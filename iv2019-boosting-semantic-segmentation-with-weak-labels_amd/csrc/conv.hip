@@ -790,6 +790,7 @@ hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t
 }
 
 hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s) {
+  if (seg_half(dtype) && conv_wgrad_patch_ok(a)) return launch_conv_wgrad_patch(dtype, a, s);
   if (seg_half(dtype) && conv_wgrad_v2_ok(a)) return launch_conv_wgrad_v2(dtype, a, s);
   if (dtype == SEG_BF16) return wg_dispatch<bf16_t>(a, s);
   if (dtype == SEG_F16) return wg_dispatch<f16_t>(a, s);

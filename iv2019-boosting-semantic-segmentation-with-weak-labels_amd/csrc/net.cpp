@@ -435,6 +435,12 @@ int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false, int k = 0)
   long P = (long)L.N * L.Ho * L.Wo;
   if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, k * k * ci, P, &BM, &BN);
   long tiles = (long)((L.co_pad + BM - 1) / BM) * ((k * k * ci + BN - 1) / BN);
+  // the small-channel 3 x 3 patch kernel (conv_wgrad_patch_ok): one 64 x 9 x 64 block per
+  // (co, ci) pair of 64-channel slices
+  if (k == 3 && L.stride == 1 && L.rate <= 4 && L.pad_h == L.rate && L.pad_w == L.rate &&
+      L.H == L.Ho && L.W == L.Wo && L.Wo % 64 == 0 && ci % 64 == 0 && ci <= 128 &&
+      L.co_pad % 64 == 0 && L.co_pad <= 128)
+    tiles = (long)(L.co_pad / 64) * (ci / 64);
   // workgroups = tiles x splits <= one wave of the CUs the launch may use; each split >= 32
   // K-steps of 64 pixels beside the dgrad chain, >= 16 alone
   const long target = concurrent ? 128 : 256;
@@ -2129,6 +2135,7 @@ int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, 
   if (ho != Ho || wo != Wo) return set_err(nullptr, -EINVAL, "wgrad geometry mismatch");
   ConvL L;
   L.co_pad = Co; L.co = Co; L.ci = Ci; L.k = k; L.N = N; L.Ho = Ho; L.Wo = Wo;
+  L.H = H; L.W = W; L.stride = stride; L.rate = rate; L.pad_h = ph; L.pad_w = pw;
   WgradArgs a{};
   a.dy = dy; a.lddy = lddy; a.x = x; a.N = N; a.H = H; a.W = W; a.C = Ci; a.ldx = ldx;
   a.Ho = Ho; a.Wo = Wo; a.Co = Co; a.KH = a.KW = k; a.sf = stride; a.pad_h = ph; a.pad_w = pw;

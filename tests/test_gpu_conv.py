@@ -170,6 +170,41 @@ def test_conv_wgrad(cuda, dtype, case):
     assert _rel(dw.cpu().numpy(), ref) < TOL[dtype]
 
 
+# small-channel 3x3 stride-1 weight gradient on input patches (wgrad_patch.hip): 64-pixel row
+# strips, 64-channel co / ci blocks, dilation <= 4, padding rows and columns at every border
+WGRAD_PATCH_CASES = [
+    (1, 8, 128, 128, 128, 3, 1, 1, False),    # 2 x 2 channel blocks, two strips per row
+    (2, 6, 64, 64, 128, 3, 1, 2, False),      # rate 2, Co 128 / Ci 64
+    (1, 5, 64, 128, 64, 3, 1, 4, False),      # rate 4 (widest patch), Ci 128 / Co 64
+    (3, 1, 192, 64, 64, 3, 1, 1, False),      # one output row per image (all taps padded)
+]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", WGRAD_PATCH_CASES)
+def test_conv_wgrad_patch(cuda, dtype, case):
+    from seg_hip import LIB, check
+    N, H, W, Ci, Co, k, s, r, ep = case
+    x, w = _tensors(case)
+    spec, Ho, Wo = _geom(case)
+    assert (Ho, Wo) == (H, W) and Wo % 64 == 0
+    g = _round(np.random.default_rng(5).standard_normal((N, Ho, Wo, Co)).astype(np.float32), dtype)
+    x = _round(x, dtype)
+    wt = torch.as_tensor(w, dtype=torch.float64).requires_grad_(True)
+    y = conv_tf(torch.as_tensor(x, dtype=torch.float64).permute(0, 3, 1, 2), wt, spec)
+    y.backward(torch.as_tensor(g, dtype=torch.float64).permute(0, 3, 1, 2))
+    ref = wt.grad.numpy()
+    xd = torch.as_tensor(x).to(cuda, TDT[dtype]).contiguous()
+    gd = torch.as_tensor(g).to(cuda, TDT[dtype]).contiguous()
+    dw = torch.zeros((Co, k, k, Ci), dtype=torch.float32, device=cuda)
+    ws = torch.zeros(64 << 20, dtype=torch.uint8, device=cuda)
+    check(LIB.seg_op_conv_wgrad(ABI[dtype], gd.data_ptr(), N, Ho, Wo, Co, Co,
+                                xd.data_ptr(), H, W, Ci, Ci, k, s, r, int(ep), dw.data_ptr(),
+                                ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert _rel(dw.cpu().numpy(), ref) < TOL[dtype]
+
+
 WGRAD_CFG_CASES = [
     # case (N, H, W, Ci, Co, k, stride, rate, explicit_pad), bm, bn, splits
     ((1, 8, 72, 256, 256, 3, 1, 2, False), 256, 256, 3),   # ping-pong, Wo >= 64 (row carries)
