@@ -35,6 +35,10 @@ struct ConvArgs {
   int ldx2, C2;
   const void* w2;
   int ldw2;
+  // optional ReLU bits of the output's consumer, [M][ldm] bytes (bit e of byte n/8 = channel n):
+  // outputs whose bit is 0 are stored as zero (conv_nt_omask_ok launches only)
+  const uint8_t* omask;
+  int ldm;
 };
 
 struct WgradArgs {
@@ -76,6 +80,9 @@ hipError_t launch_conv_skinny(int dtype, const ConvArgs& a, hipStream_t s);
 // ping-pong 256x256 main loop (conv_pp.hip) for the v2 cases with Co > 128
 bool conv_nt_pp_ok(const ConvArgs& a);
 hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s);
+// launches that apply ConvArgs::omask: 16-bit dense 1x1 ping-pong with a residual (one tile per
+// workgroup), i.e. the identity units' conv1 data gradient
+bool conv_nt_omask_ok(int dtype, const ConvArgs& a);
 // ping-pong 256x256 weight gradient (conv_pp.hip), used when the v2 tile choice is 256 x 256
 bool conv_wgrad_pp_ok(const WgradArgs& a);
 hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s);

@@ -776,6 +776,7 @@ bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a) {
 }
 
 hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t s) {
+  if (a.omask && (out_f32 || !conv_nt_omask_ok(dtype, a))) return hipErrorInvalidValue;
   if (conv_nt_uses_v2(dtype, out_f32, a)) return launch_conv_nt_v2(dtype, a, s);
   if (conv_skinny_ok(dtype, out_f32, a)) return launch_conv_skinny(dtype, a, s);
   if (dtype == SEG_BF16) {

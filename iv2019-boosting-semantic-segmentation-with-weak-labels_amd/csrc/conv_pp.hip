@@ -327,6 +327,23 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     issue_half(0, t0, 3);
     issue_half(0, t0, 1);
   };
+  // consumer ReLU bits (ConvArgs::omask, one-tile launches): one byte per 16-B chunk the
+  // epilogue stores (rows k * 32 + tid / 16, chunk tid % 16 of each 128-column half), loaded
+  // before the first K-tile so their latency hides behind the main loop (loaded in the
+  // epilogue, their latency cost ~4 us per tile: block4 conv1 dgrad +20 %)
+  uint32_t mb[2][8];
+  const bool omask = !PERSIST && a.omask;   // wave-uniform
+  if (omask) {
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const long m = m0 + k * 32 + (tid >> 4);
+        const int n = n0 + qn * 128 + (tid & 15) * 8;
+        mb[qn][k] = m < M && n < a.Co ? a.omask[(size_t)m * a.ldm + (n >> 3)] : 0u;
+      }
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads here, ahead of the prologue's DMA
+  }
   prologue();
   int dbg_it = 0; (void)dbg_it;
   for (;;) {   // ---- persistent tile loop ----
@@ -527,6 +544,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     char* const stg = smem + BUF;
     E* Y = (E*)a.y;
     const int s_row = tid >> 4, s_ch = tid & 15;
+
     // residuals (dgrad: dx = dgrad + r1 [+ r2]) are added to the fp32 accumulators before the
     // one rounding, loaded in the accumulator layout (8 B per lane, 8 fragments at a time;
     // rows past M and channels past Co clamped)
@@ -588,6 +606,15 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         v[k] = *(const u32x4_t*)(stg + row * 256 + ((s_ch ^ (row & 15)) << 4));
       }
       const int n = n0 + qn * 128 + s_ch * 8;
+      if (omask) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t b = mb[qn][k] >> (2 * w);
+            v[k][w] &= ((b & 1u) ? 0x0000ffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
+          }
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const long m = m0 + k * 32 + s_row;
@@ -663,6 +690,12 @@ bool conv_nt_pp_ok(const ConvArgs& a) {
                     a.H == a.Ho && a.W == a.Wo && a.C % 64 == 0 && a.C2 % 64 == 0 && a.ldx2 % 8 == 0 &&
                     a.ldw2 % 8 == 0 && (long)a.N * a.H * a.W * a.ldx2 * 2 < (1L << 31) &&
                     (long)a.Co * a.ldw2 * 2 < (1L << 31) && !a.r && !a.r2));
+}
+
+bool conv_nt_omask_ok(int dtype, const ConvArgs& a) {
+  return seg_half(dtype) && !a.tap8 && a.st == 1 && a.KH == 1 && a.KW == 1 && a.sf == 1 &&
+         a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho && a.W == a.Wo && !a.x2 && (a.r || a.r2) &&
+         a.Co > 128 && conv_nt_pp_ok(a) && a.ldm >= a.Co / 8;
 }
 
 template <typename E>

@@ -79,6 +79,9 @@ struct Unit {
   Act z1, z2;         // post BN+ReLU of conv1/conv2
   Act dz1, dz2, dpre; // gradients; dpre = relu-masked gradient of out (identity/subsample)
   Act dout;           // gradient wrt out (owned)
+  // this step's dout was written already ReLU-masked by the next unit's conv1 data gradient
+  // (unit_backward): the c3 BN backward reads it without the bits and dout serves as dpre
+  bool dout_masked = false;
 };
 
 struct Prof {
@@ -726,10 +729,12 @@ int gn_backward(Step& S, int li, const Act& dz0, int dz_f32, const Act* z0, cons
 ConvArgs dgrad_args(seg_ctx* c, int li, const Act& dx, const Act* r1, const Act* r2);
 
 // dx = dgrad(dy) [+ r1] [+ r2]
-int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr) {
+int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr,
+               const uint8_t* omask = nullptr) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
   ConvArgs a = dgrad_args(c, li, dx, r1, r2);
+  if (omask) { a.omask = omask; a.ldm = a.Co / 8; }
   long M = (long)L.N * L.H * L.W;
   int slot;
   // dy + w + dx (+ each residual read once)
@@ -1232,19 +1237,36 @@ int unit_forward(Step& S, Unit& u) {
   return bn_apply(S, u.c3, u.out, 0, &u.in, u.kind == SC_SUBSAMPLE ? u.stride : 1, -1, 1);
 }
 
-int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
+// pred = the unit whose output is u's input (nullptr: none). When both are identity units,
+// u's conv1 data gradient (+ the residual dpre) is stored already masked by pred's output ReLU
+// bits: everything that reads pred's dout wants it masked (pred's c3 BN backward and, as
+// pred's dpre, pred's own conv1 residual), so pred's c3 BN backward neither reads the bits nor
+// writes dpre (one M x C store pass fewer per such unit)
+bool premask_ok(seg_ctx* c, const Unit& u, const Unit* pred, bool accumulate) {
+  if (!pred || accumulate || u.kind != SC_IDENTITY || pred->kind != SC_IDENTITY || c->gn) return false;
+  if (!pred->out.mask || pred->out.C != c->convs[u.c1].ci || c->convs[pred->c3].co != pred->out.C) return false;
+  ConvArgs a = dgrad_args(c, u.c1, pred->dout, &u.dpre, nullptr);
+  a.ldm = a.Co / 8;
+  return conv_nt_omask_ok(c->dt, a);
+}
+
+int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred = nullptr) {
   seg_ctx* c = S.c;
   // identity / subsample shortcuts: the c3 BN backward also writes the ReLU-masked dout
-  // (dpre), the residual of the unit's input gradient. (Measured and rejected: folding the
-  // mask into conv1's dgrad epilogue instead, 1.8 % slower per step.)
-  const Act* dpre = u.kind != SC_CONV ? &u.dpre : nullptr;
+  // (dpre), the residual of the unit's input gradient -- unless dout arrived masked
+  // (dout_masked, premask_ok). (Measured and rejected: reading dout + the bits as the
+  // residual in conv1's dgrad epilogue instead of dpre, 1.8 % slower per step.)
+  const bool in_masked = u.dout_masked;
+  u.dout_masked = false;
+  const Act* dpre = u.kind != SC_CONV && !in_masked ? &u.dpre : nullptr;
+  const Act& dres = in_masked ? u.dout : u.dpre;   // the masked dout, wherever it lives
   const ConvL& L3 = c->convs[u.c3];
   const ConvL& Ls = c->convs[u.kind == SC_CONV ? u.sc : u.c3];
   if (u.kind == SC_CONV && !c->gn && !c->sync_fn && u.out.mask && u.out.C == L3.co &&
       Ls.co == L3.co && Ls.rb == L3.rb && Ls.y.M() == L3.y.M()) {
     if (int r = bn_backward_dual(S, u.c3, u.sc, u.dout, u.out)) return r;
   } else {
-    if (int r = bn_backward(S, u.c3, u.dout, 0, &u.out, dpre)) return r;
+    if (int r = bn_backward(S, u.c3, u.dout, 0, in_masked ? nullptr : &u.out, dpre)) return r;
     if (u.kind == SC_CONV)
       if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
   }
@@ -1257,13 +1279,17 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate) {
   if (int r = conv_wgrad(S, u.c1, u.in)) return r;
   switch (u.kind) {
     case SC_IDENTITY:
-      if (accumulate) return conv_dgrad(S, u.c1, dx, &dx, &u.dpre);
-      return conv_dgrad(S, u.c1, dx, &u.dpre);
+      if (accumulate) return conv_dgrad(S, u.c1, dx, &dx, &dres);
+      if (premask_ok(c, u, pred, accumulate)) {
+        pred->dout_masked = true;
+        return conv_dgrad(S, u.c1, dx, &dres, nullptr, pred->out.mask);
+      }
+      return conv_dgrad(S, u.c1, dx, &dres);
     case SC_SUBSAMPLE: {
       if (accumulate) return set_err(&c->err, -EINVAL, "accumulating subsample unit");
       if (int r = conv_dgrad(S, u.c1, dx)) return r;
-      HIPCALL(c, launch_add_strided(S.dt, dx.p, dx.H, dx.W, dx.ld, u.dpre.p, u.dpre.N, u.dpre.H,
-                                    u.dpre.W, u.dpre.C, u.dpre.ld, u.stride, S.s));
+      HIPCALL(c, launch_add_strided(S.dt, dx.p, dx.H, dx.W, dx.ld, dres.p, dres.N, dres.H,
+                                    dres.W, dres.C, dres.ld, u.stride, S.s));
       return 0;
     }
     case SC_CONV: {
@@ -1495,7 +1521,7 @@ int backward_layers(Step& S) {
   if (int r = conv_dgrad(S, c->dfd, c->units.back().dout)) return r;
   for (int i = (int)c->units.size() - 1; i >= 0; --i) {
     const Act& dx = i == 0 ? c->dp0 : c->units[i - 1].dout;
-    if (int r = unit_backward(S, c->units[i], dx, false)) return r;
+    if (int r = unit_backward(S, c->units[i], dx, false, i == 0 ? nullptr : &c->units[i - 1])) return r;
   }
   HIPCALL(c, launch_maxpool_bwd(S.dt, c->pool_arg, c->z0.N, c->z0.H, c->z0.W, 64, c->dp0.p,
                                 c->dp0.H, c->dp0.W, c->dp0.ld, c->dz0.p, c->dz0.ld, c->pool_ph,
