@@ -115,6 +115,12 @@ int seg_set_nesterov(seg_ctx* ctx, int on);
  * it and joins before the stem's weights. Every other call that takes a stream joins first.
  * No reference counterpart (scheduling only; results are unchanged). Off by default. */
 int seg_set_defer_stem(seg_ctx* ctx, int on);
+/* pre-masked identity-unit gradients (on by default): when an identity unit follows another,
+ * its conv1 data gradient stores the previous unit's output gradient already ReLU-masked, and
+ * that unit's c3 BN backward skips the mask bits and the separate masked-gradient store.
+ * Scheduling of bytes only: results are bitwise identical either way (tests/test_gpu_step.py).
+ * No reference counterpart. */
+int seg_set_premask(seg_ctx* ctx, int on);
 
 /* outputs ------------------------------------------------------------------------------
  * losses: device float[10] = {segmentation, l1, l2_vehicle, l2_human, n1, n2v, n2h,

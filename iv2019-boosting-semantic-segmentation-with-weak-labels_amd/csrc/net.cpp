@@ -201,6 +201,7 @@ struct seg_ctx {
   // parameter beside that last kernel and joins (ev_join) before the stem's weights
   hipEvent_t ev_prestem = nullptr;
   bool defer_stem = false;
+  bool premask = true;             // seg_set_premask: pre-masked identity-unit gradients (unit_backward)
   bool prestem_rec = false;
   bool stem_pending = false;
   float* dzscale = nullptr;       // [ldl]
@@ -1243,7 +1244,8 @@ int unit_forward(Step& S, Unit& u) {
 // pred's dpre, pred's own conv1 residual), so pred's c3 BN backward neither reads the bits nor
 // writes dpre (one M x C store pass fewer per such unit)
 bool premask_ok(seg_ctx* c, const Unit& u, const Unit* pred, bool accumulate) {
-  if (!pred || accumulate || u.kind != SC_IDENTITY || pred->kind != SC_IDENTITY || c->gn) return false;
+  if (!c->premask || !pred || accumulate || u.kind != SC_IDENTITY || pred->kind != SC_IDENTITY || c->gn)
+    return false;
   if (!pred->out.mask || pred->out.C != c->convs[u.c1].ci || c->convs[pred->c3].co != pred->out.C) return false;
   ConvArgs a = dgrad_args(c, u.c1, pred->dout, &u.dpre, nullptr);
   a.ldm = a.Co / 8;
@@ -1850,6 +1852,12 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
 int seg_set_defer_stem(seg_ctx* c, int on) {
   if (!c) return set_err(nullptr, -EINVAL, "null ctx");
   c->defer_stem = on != 0;
+  return 0;
+}
+
+int seg_set_premask(seg_ctx* c, int on) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  c->premask = on != 0;
   return 0;
 }
 

@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = [
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
     "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict", "seg_full_predictions",
-    "seg_set_nesterov", "seg_set_defer_stem",
+    "seg_set_nesterov", "seg_set_defer_stem", "seg_set_premask",
     "seg_crc32c", "seg_prepare_images", "seg_prepare_labels", "seg_prepare_images_crop",
 ]
 
@@ -120,6 +120,7 @@ def _load():
         "seg_full_predictions": (ip, [vp, vp, vp, vp, vp, vp]),
         "seg_set_nesterov": (ip, [vp, ip]),
         "seg_set_defer_stem": (ip, [vp, ip]),
+        "seg_set_premask": (ip, [vp, ip]),
     }
     override = "SEG_HIP_LIB" in os.environ   # A/B builds of older commits may lack new entries
     for name, (res, args) in sig.items():
@@ -359,6 +360,10 @@ class SegContext:
         gradient (the step's last kernel); gradients must not be read between backward() and
         apply_update() while this is on."""
         check(LIB.seg_set_defer_stem(self.h, 1 if on else 0), self.h)
+
+    def set_premask(self, on):
+        """seg_set_premask: pre-masked identity-unit gradients (default on; results unchanged)."""
+        check(LIB.seg_set_premask(self.h, 1 if on else 0), self.h)
 
     def apply_update(self, lr, momentum=0.9, ema_decay_eff=0.0, grad_scale=1.0, stream=None):
         check(LIB.seg_apply_update(self.h, lr, momentum, ema_decay_eff, grad_scale,

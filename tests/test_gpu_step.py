@@ -245,6 +245,49 @@ def test_defer_stem_update_matches(cuda, dtype):
     assert np.allclose(r0, r1, rtol=1e-6), (r0, r1)
 
 
+@pytest.mark.parametrize("dtype,depth", [("bf16", 50), ("fp16", 101)])
+def test_premask_matches(cuda, dtype, depth):
+    """seg_set_premask (identity units' conv1 data gradient stores the previous unit's output
+    gradient already ReLU-masked; that unit's c3 BN backward then reads it without the bits and
+    writes no separate masked copy): three steps give bitwise the same losses, gradients,
+    parameters and momentum as the path that masks in the BN backward."""
+    from input_pipelines.synthetic import batch
+    from seg_hip import SegContext
+    cfg = SegConfig(depth=depth, height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=11).items()}
+    data = batch(23, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
+    img = torch.as_tensor(data["images"]).to(cuda)
+    px = torch.as_tensor(data["px"]).to(cuda)
+    bb = torch.as_tensor(data["bbox"]).to(cuda)
+    out = []
+    for pm in (False, True):
+        ctx = SegContext(depth=depth, pyramid=cfg.pyramid, height=cfg.height, width=cfg.width,
+                         nb_pp=1, nb_pb=1, dtype=dtype)
+        ctx.load_params(params)
+        if dtype == "fp16":
+            ctx.set_loss_scale(1024.0)
+        ctx.set_premask(pm)
+        losses = []
+        for step in range(3):
+            ctx.forward(img)
+            ctx.loss(px, bb, None)
+            ctx.backward()
+            torch.cuda.synchronize()
+            grads = ctx.named("grads")
+            ctx.apply_update(0.01, 0.9)
+            torch.cuda.synchronize()
+            losses.append(ctx.outputs()[0].cpu().numpy().copy())
+        out.append((losses, grads, ctx.named("params"), ctx.momentum.cpu().numpy().copy()))
+        ctx.close()
+    (l0, g0, p0, m0), (l1, g1, p1, m1) = out
+    assert all(np.array_equal(a, b) for a, b in zip(l0, l1))
+    for k in g0:
+        assert np.array_equal(g0[k], g1[k]), k
+    for k in p0:
+        assert np.array_equal(p0[k], p1[k]), k
+    assert np.array_equal(m0, m1)
+
+
 def test_defer_stem_join_on_other_stream(cuda):
     """with defer on, a join-taking call on another stream (seg_predict on B) between
     seg_backward and seg_apply_update (both on A) must not consume the pending stem join: the
