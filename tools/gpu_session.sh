@@ -1,9 +1,11 @@
+# One GPU-box pass for the round's final record: the driver's GPU suite, smoke and the full
+# default bench line (rocprofv3 / PMC passes: tools/measure_round.sh). Every step has its own
+# time limit and the chain stops at the first failure.
 set -e
-out=gpurun_out/s13
+out=gpurun_out/m3
 mkdir -p $out
 export TMPDIR=/tmp
-echo parity; timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_conv.py -k "wgrad" > $out/parity.txt 2>&1
-echo ops; OPS="wgrad" LAYERS="b1c2 b2c2" timeout -k 10 300 tools/ab_ops.sh base > $out/ops.txt 2>&1
-echo full; timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_fullsize.py > $out/full.txt 2>&1
-echo ab; timeout -k 10 600 tools/ab_bench.sh base > $out/ab.txt 2>&1
+echo suite; timeout -k 10 600 python3 -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests > $out/suite.txt 2>&1
+echo smoke; timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
+echo bench; timeout -k 10 400 python3 -u bench.py --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.err
 echo done
