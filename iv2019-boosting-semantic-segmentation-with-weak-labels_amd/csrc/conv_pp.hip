@@ -60,6 +60,19 @@ constexpr int PP_LDS = 2 * BUF;            // 128 KB
 
 __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
 
+template <typename E> __device__ __forceinline__ E lo16(uint32_t w) {
+  const uint16_t b = (uint16_t)(w & 0xffffu);
+  E e;
+  __builtin_memcpy(&e, &b, 2);
+  return e;
+}
+template <typename E> __device__ __forceinline__ E hi16(uint32_t w) {
+  const uint16_t b = (uint16_t)(w >> 16);
+  E e;
+  __builtin_memcpy(&e, &b, 2);
+  return e;
+}
+
 // compiler fences around the raw barrier: nothing moves across it (IR or machine schedule)
 __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
@@ -545,55 +558,38 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     E* Y = (E*)a.y;
     const int s_row = tid >> 4, s_ch = tid & 15;
 
-    // residuals (dgrad: dx = dgrad + r1 [+ r2]) are added to the fp32 accumulators before the
-    // one rounding, loaded in the accumulator layout (8 B per lane, 8 fragments at a time;
-    // rows past M and channels past Co clamped)
+    // residuals (dgrad: dx = dgrad + r1 [+ r2]; one-tile launches only, pp_launch_st) are read
+    // in the staged layout -- 16 B per lane, 256 contiguous bytes per row, issued before the
+    // half's staging writes -- and added after the LDS round trip, in fp32, rounded once more
+    // (round 3: they were read in the accumulator layout, 8 B per lane from 16 rows per load,
+    // a quadrant at a time, and added before the single rounding: the short-K residual data
+    // gradients 6-8 % slower, the step -0.6 %; profiles/r03_res_staged.txt)
     const E* R1 = (const E*)a.r;
     const E* R2 = (const E*)a.r2;
-    // (persistent launches carry no residuals: pp_launch_st routes those to PERSIST = 0, whose
-    // register budget has room for the residual loads; a persistent variant with residuals
-    // spilled 3 registers and was no faster)
     const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
-    auto add4 = [](f32x4_t& v, const uint2 u) {
-      const uint32_t w[2] = {u.x, u.y};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint16_t bl = (uint16_t)(w[h] & 0xffffu), bh = (uint16_t)(w[h] >> 16);
-        E lo, hi;
-        __builtin_memcpy(&lo, &bl, 2);
-        __builtin_memcpy(&hi, &bh, 2);
-        v[2 * h] += TypeOps<E>::to_f(lo);
-        v[2 * h + 1] += TypeOps<E>::to_f(hi);
-      }
-    };
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn) {
+      u32x4_t rs1[8], rs2[8];
+      if (nres) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const long m = m0 + k * 32 + s_row;
+          const long mc = m < M ? m : M - 1;
+          const int n = n0 + qn * 128 + s_ch * 8;
+          const int nc = n < a.Co ? n : 0;
+          rs1[k] = *(const u32x4_t*)(R1 + (size_t)mc * a.ldr + nc);
+          if (nres == 2) rs2[k] = *(const u32x4_t*)(R2 + (size_t)mc * a.ldr2 + nc);
+        }
+      }
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
-        uint2 r1v[4][2], r2v[4][2];
-        if (nres) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const long m = mw + qm * 64 + i * 16 + lr;
-              const long mc = m < M ? m : M - 1;
-              const int n = nbase + qn * 128 + j * 16;
-              const int nc = n < a.Co ? n : 0;
-              r1v[i][j] = *(const uint2*)(R1 + (size_t)mc * a.ldr + nc);
-              if (nres == 2) r2v[i][j] = *(const uint2*)(R2 + (size_t)mc * a.ldr2 + nc);
-            }
-        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int row = wm * 128 + qm * 64 + i * 16 + lr;
             const int ch = wn * 4 + j * 2 + (lq >> 1);
-            f32x4_t v = acc[qm][qn][i][j];
-            if (nres) add4(v, r1v[i][j]);
-            if (nres == 2) add4(v, r2v[i][j]);
-            *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) = pack4(v);
+            *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) = pack4(acc[qm][qn][i][j]);
           }
       }
       if (a.stats && nvalid > 0) stats_half(qn);
@@ -606,6 +602,18 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         v[k] = *(const u32x4_t*)(stg + row * 256 + ((s_ch ^ (row & 15)) << 4));
       }
       const int n = n0 + qn * 128 + s_ch * 8;
+      if (nres) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t x = v[k][w], r = rs1[k][w], r2 = nres == 2 ? rs2[k][w] : 0u;
+            float lo = TypeOps<E>::to_f(lo16<E>(x)) + TypeOps<E>::to_f(lo16<E>(r));
+            float hi = TypeOps<E>::to_f(hi16<E>(x)) + TypeOps<E>::to_f(hi16<E>(r));
+            if (nres == 2) { lo += TypeOps<E>::to_f(lo16<E>(r2)); hi += TypeOps<E>::to_f(hi16<E>(r2)); }
+            v[k][w] = pack4(f32x4_t{lo, hi, 0.f, 0.f})[0];
+          }
+      }
       if (omask) {
 #pragma unroll
         for (int k = 0; k < 8; ++k)
