@@ -121,6 +121,10 @@ int seg_set_defer_stem(seg_ctx* ctx, int on);
  * Scheduling of bytes only: results are bitwise identical either way (tests/test_gpu_step.py).
  * No reference counterpart. */
 int seg_set_premask(seg_ctx* ctx, int on);
+/* runtime counters since seg_create (diagnostics; no reference counterpart):
+ * "premask_launches" = conv1 data gradients stored pre-masked (seg_set_premask).
+ * -ENOENT for an unknown name. */
+int seg_counter(seg_ctx* ctx, const char* name, int64_t* value);
 
 /* outputs ------------------------------------------------------------------------------
  * losses: device float[10] = {segmentation, l1, l2_vehicle, l2_human, n1, n2v, n2h,

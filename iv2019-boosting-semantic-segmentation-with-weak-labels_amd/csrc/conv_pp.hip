@@ -269,28 +269,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   f32x4_t acc[2][2][4][2];   // [qm][qn][fi][fj]
 
   V af[4][2], bfq[2][2][2];   // [frag][k-half]; B per quadrant qn: B0 kept for phase 3
-#ifdef NT_DBG_AFOLD
-  // A/B diagnostic only (wrong results): the cost of folding the producer's BN apply + ReLU
-  // into this conv's A operand in registers (per-lane scale / shift of its 8 channels)
-  float fs[8], fb[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) { fs[c] = 1.f + 1e-3f * (float)(lane + c); fb[c] = -1e-3f * (float)(c + lq); }
-  auto fold = [&](V& f) {
-    uint32_t w[4];
-    __builtin_memcpy(w, &f, 16);
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const float lo = fmaxf(fmaf(__uint_as_float(w[h] << 16), fs[2 * h], fb[2 * h]), 0.f);
-      const float hi = fmaxf(fmaf(__uint_as_float(w[h] & 0xffff0000u), fs[2 * h + 1], fb[2 * h + 1]), 0.f);
-      const E el = TypeOps<E>::from_f(lo), eh = TypeOps<E>::from_f(hi);
-      uint16_t bl, bh;
-      __builtin_memcpy(&bl, &el, 2);
-      __builtin_memcpy(&bh, &eh, 2);
-      w[h] = (uint32_t)bl | ((uint32_t)bh << 16);
-    }
-    __builtin_memcpy(&f, w, 16);
-  };
-#endif
   auto read_a = [&](const char* buf, int qm) {
     const char* A = buf + qm * HALF;
 #pragma unroll
@@ -299,12 +277,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) af[i][s] = *(const V*)(A + row * 128 + swz(row, lq + 4 * s) * 16);
     }
-#ifdef NT_DBG_AFOLD
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) fold(af[i][s]);
-#endif
   };
   auto read_b = [&](const char* buf, int qn) {
     const char* B = buf + (2 + qn) * HALF;
@@ -891,28 +863,14 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       auto* ldst = (__attribute__((address_space(3))) void*)(dst + (i * 8 + wave) * 1024);
       if (hid < 2) {
         const int j = hid * 2 + i;
-        uint32_t off = r_[i] < cur_prem ? a_voff[j] + (uint32_t)(cur_p0 * a.lddy * 2) : OOB;
-#ifdef WG_DBG_SAMELINE   // A/B diagnostics only (wrong results): every row reads the tile's row 0
-        off = a_voff[j] - (uint32_t)(r_[i] * a.lddy * 2);
-#endif
-#ifndef WG_DBG_NODMA
+        const uint32_t off = r_[i] < cur_prem ? a_voff[j] + (uint32_t)(cur_p0 * a.lddy * 2) : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_dy, ldst, 16, off, 0, 0, 0);
-#else
-        (void)off; (void)ldst;
-#endif
       } else {
         const int j = (hid - 2) * 2 + i;
         const int hi = hb[i] + b_dh[j], wi = wb[i] + b_dw[j];
         const bool ok = pv[i] & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
-        uint32_t off = ok ? (uint32_t)((pixb[i] + b_toff[j]) * 2) : OOB;
-#ifdef WG_DBG_SAMELINE
-        off = (uint32_t)(b_toff[j] > 0 ? b_toff[j] * 2 : 0);
-#endif
-#ifndef WG_DBG_NODMA
+        const uint32_t off = ok ? (uint32_t)((pixb[i] + b_toff[j]) * 2) : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, ldst, 16, off, 0, 0, 0);
-#else
-        (void)off; (void)ldst;
-#endif
       }
     }
   };
@@ -1087,12 +1045,6 @@ __global__ __launch_bounds__(PP_THREADS, 1) void conv_wgrad_pp_kernel(WgradArgs 
 
 }  // namespace
 
-// A/B switch read once per process (experiments only)
-static bool getenv_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && v[0] == '1';
-}
-
 // 256 x 256 wgrad tiles with operands < 2^31 bytes (32-bit buffer offsets)
 bool conv_wgrad_pp_ok(const WgradArgs& a) {
   const long P = (long)a.N * a.Ho * a.Wo;
@@ -1111,7 +1063,7 @@ hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s) {
   };
   // strip order where the rows split into whole 64-pixel K-tiles and the pixel rows repeat
   // across taps (KH > 1); 1x1 layers read every x row once, raster order is as good there
-  const bool strip = (a.Wo % 64) == 0 && a.KH > 1 && !getenv_flag("SEG_WGRAD_RASTER");
+  const bool strip = (a.Wo % 64) == 0 && a.KH > 1;
   if (dtype == SEG_F16) {
     if (strip) return launch(conv_wgrad_pp_kernel<f16_t, 2>);
     if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<f16_t, 1>);

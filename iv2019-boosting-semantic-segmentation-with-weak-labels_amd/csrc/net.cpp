@@ -202,6 +202,7 @@ struct seg_ctx {
   hipEvent_t ev_prestem = nullptr;
   bool defer_stem = false;
   bool premask = true;             // seg_set_premask: pre-masked identity-unit gradients (unit_backward)
+  int64_t premask_launches = 0;    // conv1 data gradients stored pre-masked (seg_counter)
   bool prestem_rec = false;
   bool stem_pending = false;
   float* dzscale = nullptr;       // [ldl]
@@ -431,20 +432,15 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
 // whole second wave for the few: tools/wgrad_sweep.py PP_ONLY=1 on the C2 shapes, e.g. block3
 // 3x3 (9 tiles) 24 splits 188 us, 32 splits (288 workgroups) 266 us; block3 1x1 (4 tiles) 64
 // splits 97 us against the former 2-wave 128 splits 121 us.
-int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false, int k = 0) {
-  if (!ci) ci = L.ci;   // 16 for the space-to-depth stem
-  if (!k) k = L.k;      // 4 for the space-to-depth stem
-  int BM = L.co_pad <= 64 ? 64 : 128;
+int wgrad_splits(const WgradArgs& a, int dt, bool concurrent = false) {
+  const int ci = a.C, k = a.KH, co = a.Co;   // Co = co_pad; 16 / 4 for the space-to-depth stem
+  int BM = co <= 64 ? 64 : 128;
   int BN = 128;
-  long P = (long)L.N * L.Ho * L.Wo;
-  if (ci % 8 == 0) conv_wgrad_v2_tile(L.co_pad, k * k * ci, P, &BM, &BN);
-  long tiles = (long)((L.co_pad + BM - 1) / BM) * ((k * k * ci + BN - 1) / BN);
-  // the small-channel 3 x 3 patch kernel (conv_wgrad_patch_ok): one 64 x 9 x 64 block per
-  // (co, ci) pair of 64-channel slices
-  if (k == 3 && L.stride == 1 && L.rate <= 4 && L.pad_h == L.rate && L.pad_w == L.rate &&
-      L.H == L.Ho && L.W == L.Wo && L.Wo % 64 == 0 && ci % 64 == 0 && ci <= 128 &&
-      L.co_pad % 64 == 0 && L.co_pad <= 128)
-    tiles = (long)(L.co_pad / 64) * (ci / 64);
+  long P = (long)a.N * a.Ho * a.Wo;
+  if (ci % 8 == 0) conv_wgrad_v2_tile(co, k * k * ci, P, &BM, &BN);
+  long tiles = (long)((co + BM - 1) / BM) * ((k * k * ci + BN - 1) / BN);
+  // the small-channel 3 x 3 patch kernel: the same predicate launch_conv_wgrad dispatches on
+  if (seg_half(dt) && conv_wgrad_patch_ok(a)) tiles = conv_wgrad_patch_blocks(a);
   // workgroups = tiles x splits <= one wave of the CUs the launch may use; each split >= 32
   // K-steps of 64 pixels beside the dgrad chain, >= 16 alone
   const long target = concurrent ? 128 : 256;
@@ -452,6 +448,18 @@ int wgrad_splits(const ConvL& L, int ci = 0, bool concurrent = false, int k = 0)
   long maxs = std::max<long>(1, P / (concurrent ? 2048 : 1024));
   s = std::min(s, maxs);
   return (int)std::min<long>(s, 256);
+}
+
+// the weight-gradient problem of layer L (x / dy pixel strides: the activations' layout,
+// channels padded to a multiple of 8); the space-to-depth stem is a 4 x 4 VALID conv over 16
+// channels
+WgradArgs wgrad_problem(const ConvL& L, bool s2d) {
+  WgradArgs a{};
+  a.N = L.N; a.H = L.H; a.W = L.W; a.C = s2d ? 16 : L.ci; a.ldx = (a.C + 7) / 8 * 8;
+  a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co_pad; a.lddy = (L.co_pad + 7) / 8 * 8;
+  a.KH = a.KW = s2d ? 4 : L.k; a.sf = s2d ? 1 : L.stride; a.dil = s2d ? 1 : L.rate;
+  a.pad_h = s2d ? 0 : L.pad_h; a.pad_w = s2d ? 0 : L.pad_w;
+  return a;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -835,7 +843,11 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   // the stem's weight gradient is the last work of the step (its dgrad is skipped): nothing
   // runs beside it, so it takes the whole chip (tools/timeline.py: the compute stream idled
   // ~0.75 ms waiting for it)
-  a.splits = wgrad_splits(L, a.C, c->side_active && li != c->stem, a.KH);
+  a.splits = wgrad_splits(a, S.dt, c->side_active && li != c->stem);
+  {  // the slab was sized at creation for these shapes; never exceed it
+    const long per = (long)a.Co * a.KH * a.KW * a.C;
+    a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / per));
+  }
   a.out = c->slab;
   long P = (long)L.N * L.Ho * L.Wo;
   int slot;
@@ -1206,9 +1218,9 @@ int build(seg_ctx* c) {
     }
     if (seg_half(c->dt)) L.w_lp = (uint16_t*)c->w_lp_flat + L.w_off;   // bf16 or fp16 bits
     const bool s2d = &L == &c->convs[c->stem] && c->stem_s2d;
-    const int wci = s2d ? 16 : L.ci, wk = s2d ? 4 : L.k;
-    const int sp = std::max(wgrad_splits(L, wci, false, wk), wgrad_splits(L, wci, true, wk));
-    slab = std::max(slab, (size_t)sp * L.co_pad * wk * wk * wci);
+    const WgradArgs a = wgrad_problem(L, s2d);
+    const int sp = std::max(wgrad_splits(a, c->dt, false), wgrad_splits(a, c->dt, true));
+    slab = std::max(slab, (size_t)sp * a.Co * a.KH * a.KW * a.C);
   }
   if (c->stem_s2d) {
     const ConvL& st = c->convs[c->stem];
@@ -1283,8 +1295,10 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred =
     case SC_IDENTITY:
       if (accumulate) return conv_dgrad(S, u.c1, dx, &dx, &dres);
       if (premask_ok(c, u, pred, accumulate)) {
-        pred->dout_masked = true;
-        return conv_dgrad(S, u.c1, dx, &dres, nullptr, pred->out.mask);
+        if (int r = conv_dgrad(S, u.c1, dx, &dres, nullptr, pred->out.mask)) return r;
+        pred->dout_masked = true;   // only once the masked store is enqueued
+        ++c->premask_launches;
+        return 0;
       }
       return conv_dgrad(S, u.c1, dx, &dres);
     case SC_SUBSAMPLE: {
@@ -1451,6 +1465,9 @@ int backward(Step& S) {
 
 int backward_layers(Step& S) {
   seg_ctx* c = S.c;
+  // no pre-masked gradient survives a backward that stopped part-way (unit_backward)
+  for (auto& u : c->units) u.dout_masked = false;
+  for (auto& u : c->heads) u.dout_masked = false;
   // hybrid: the loss-normalised gradient goes back through the deconvolution first (its
   // weight / bias gradients and dx), then into the logits BN without a further scale
   if (c->hybrid) HIPCALL(c, launch_deconv_bwd(deconv_args(c), S.s));
@@ -1861,6 +1878,14 @@ int seg_set_premask(seg_ctx* c, int on) {
   return 0;
 }
 
+int seg_counter(seg_ctx* c, const char* name, int64_t* value) {
+  if (!c || !name || !value) return set_err(c ? &c->err : nullptr, -EINVAL, "null argument");
+  const std::string n(name);
+  if (n == "premask_launches") *value = c->premask_launches;
+  else return set_err(&c->err, -ENOENT, "unknown counter '%s'", name);
+  return 0;
+}
+
 int seg_outputs(seg_ctx* c, const float** losses, const float** reg, const float** logits,
                 int* ld, int* hl, int* wl) {
   if (!c) return set_err(nullptr, -EINVAL, "null ctx");
@@ -2167,13 +2192,10 @@ int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, 
   int ho, wo, ph, pw;
   op_geom(H, W, k, stride, rate, explicit_pad, &ho, &wo, &ph, &pw);
   if (ho != Ho || wo != Wo) return set_err(nullptr, -EINVAL, "wgrad geometry mismatch");
-  ConvL L;
-  L.co_pad = Co; L.co = Co; L.ci = Ci; L.k = k; L.N = N; L.Ho = Ho; L.Wo = Wo;
-  L.H = H; L.W = W; L.stride = stride; L.rate = rate; L.pad_h = ph; L.pad_w = pw;
   WgradArgs a{};
   a.dy = dy; a.lddy = lddy; a.x = x; a.N = N; a.H = H; a.W = W; a.C = Ci; a.ldx = ldx;
   a.Ho = Ho; a.Wo = Wo; a.Co = Co; a.KH = a.KW = k; a.sf = stride; a.pad_h = ph; a.pad_w = pw;
-  a.dil = rate; a.splits = wgrad_splits(L);
+  a.dil = rate; a.splits = wgrad_splits(a, dt_of(dtype));
   const long n = (long)Co * k * k * Ci;
   if ((int64_t)a.splits * n * 4 > ws_bytes) a.splits = (int)std::max<int64_t>(1, ws_bytes / (n * 4));
   a.out = (float*)workspace;

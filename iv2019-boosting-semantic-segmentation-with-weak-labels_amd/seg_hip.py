@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = [
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
     "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict", "seg_full_predictions",
-    "seg_set_nesterov", "seg_set_defer_stem", "seg_set_premask",
+    "seg_set_nesterov", "seg_set_defer_stem", "seg_set_premask", "seg_counter",
     "seg_crc32c", "seg_prepare_images", "seg_prepare_labels", "seg_prepare_images_crop",
 ]
 
@@ -121,6 +121,7 @@ def _load():
         "seg_set_nesterov": (ip, [vp, ip]),
         "seg_set_defer_stem": (ip, [vp, ip]),
         "seg_set_premask": (ip, [vp, ip]),
+        "seg_counter": (ip, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     }
     override = "SEG_HIP_LIB" in os.environ   # A/B builds of older commits may lack new entries
     for name, (res, args) in sig.items():
@@ -364,6 +365,12 @@ class SegContext:
     def set_premask(self, on):
         """seg_set_premask: pre-masked identity-unit gradients (default on; results unchanged)."""
         check(LIB.seg_set_premask(self.h, 1 if on else 0), self.h)
+
+    def counter(self, name: str) -> int:
+        """seg_counter: a runtime counter since creation (e.g. "premask_launches")."""
+        v = ctypes.c_int64()
+        check(LIB.seg_counter(self.h, name.encode(), ctypes.byref(v)), self.h)
+        return v.value
 
     def apply_update(self, lr, momentum=0.9, ema_decay_eff=0.0, grad_scale=1.0, stream=None):
         check(LIB.seg_apply_update(self.h, lr, momentum, ema_decay_eff, grad_scale,

@@ -594,7 +594,12 @@ class OracleNet:
         return d[:, hy][:, :, wx]
 
     # -- losses (define_losses_hierarchical.py:98-210) ---------------------------------
-    def losses(self, low, px_labels, bbox_soft=None, tag_soft=None):
+    def losses(self, low, px_labels, bbox_soft=None, tag_soft=None, weak_l1_decisions=None):
+        """`weak_l1_decisions` (int [Nb_pb + Nb_pi, H, W], optional) replaces this forward's
+        l1 argmax in the weak-pixel gate of the l2 weights (:169-177) -- the same weight mask
+        as another implementation's run, so that argmax near-ties do not flip pixels in and
+        out of the l2 terms when the two are compared; the losses' values and gradients are
+        still this forward's."""
         cfg = self.cfg
         t = TABLES[cfg.dataset]
         up, probs, decs, _ = self.head_predictions(low)
@@ -630,7 +635,9 @@ class OracleNet:
             if y.shape[0] > npp:
                 yw = y[npp:]
                 not_void = (1.0 - yw[..., -1]) > 0.01
-                l1c = (decs["l1_logits"][npp:] == cid_l1) & (yw[..., :-1].max(dim=-1).values >= 0.01)
+                d1w = decs["l1_logits"][npp:] if weak_l1_decisions is None else \
+                    torch.as_tensor(weak_l1_decisions, dtype=torch.long)
+                l1c = (d1w == cid_l1) & (yw[..., :-1].max(dim=-1).values >= 0.01)
                 w = torch.cat([w_strong, (not_void & l1c).to(self.dtype)], 0)
             else:
                 w = w_strong
@@ -648,15 +655,16 @@ class OracleNet:
     # -- one full training step ----------------------------------------------------------
     def train_step(self, images, px_labels, bbox_soft=None, tag_soft=None, lr=0.01,
                    momentum=0.9, mom_state=None, ema_state=None, ema_decay=0.0, step=0,
-                   nesterov=False):
+                   nesterov=False, weak_l1_decisions=None):
         """Forward, losses, autodiff backward of the segmentation loss, SGDM with L2 term
         (MomentumOptimizer, use_nesterov per define_optimizer.py:17-20).
 
         Returns (losses, grads-of-seg-loss, new params, new momentum, new ema, batch stats).
+        `weak_l1_decisions`: see losses().
         """
         trainable = self._trainable()
         low = self.forward(torch.as_tensor(images))
-        L = self.losses(low, px_labels, bbox_soft, tag_soft)
+        L = self.losses(low, px_labels, bbox_soft, tag_soft, weak_l1_decisions)
         return (L, low) + self._grads_and_update(L["segmentation"], trainable, lr, momentum,
                                                  mom_state, ema_state, ema_decay, step,
                                                  nesterov)

@@ -278,6 +278,10 @@ def test_premask_matches(cuda, dtype, depth):
             torch.cuda.synchronize()
             losses.append(ctx.outputs()[0].cpu().numpy().copy())
         out.append((losses, grads, ctx.named("params"), ctx.momentum.cpu().numpy().copy()))
+        # the pre-masked path really ran (identity-unit pairs exist in every R50/R101 block)
+        # or really did not
+        n_pm = ctx.counter("premask_launches")
+        assert (n_pm > 0) if pm else (n_pm == 0), (pm, n_pm)
         ctx.close()
     (l0, g0, p0, m0), (l1, g1, p1, m1) = out
     assert all(np.array_equal(a, b) for a, b in zip(l0, l1))
