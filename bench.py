@@ -138,6 +138,75 @@ def cpu_baseline(pyramid, reps=3):
                              "warm-up; steps " + ", ".join(f"{t:.1f}" for t in ts1) + " s"}}
 
 
+def train_py_leg(args, steps=10, warmup=3):
+    """The drop-in trainer end to end: ``train.py``'s facade
+    (SemanticSegmentation.train -> define_estimator -> model_fn / define_losses / train_op) on
+    the bench's workload, timed over `steps` steps after `warmup` (system_factory's
+    timing_warmup: synchronised clock, input pipeline included), twice:
+    * real data: a 1024 x 2048 Cityscapes-format TFRecord written here (8 records: PNG image +
+      label-id PNG, KEYS2FEATURES_v5), decoded on the host by the pool of
+      input_pipelines/train_inputs.py, preprocessed on the device;
+    * synthetic: train.synthetic_train_input's seeded batches, resident in HBM and cycled
+      (a pool of `warmup` batches, generated on the host during the warm-up steps)."""
+    import shutil
+    import tempfile
+    import numpy as np
+    import train
+    from estimator.define_estimator_hierarchical import get_or_create_global_step
+    from input_pipelines.tfrecords import encode_example, encode_png, write_records
+    from input_pipelines.train_inputs import default_workers
+    from models import resnet50_extended_model_hierarchical as mh
+    tmp = tempfile.mkdtemp(prefix="seg_trainpy_")
+    try:
+        rng = np.random.default_rng(5)
+        recs = []
+        t_gen = time.perf_counter()
+        for i in range(8):
+            # photo-like content (smooth 32 px blocks + small noise: ~3x PNG compression, as
+            # Cityscapes' leftImg8bit PNGs) and blocky label ids 0..33
+            base = rng.integers(0, 256, (H // 32, W // 32, 3), dtype=np.uint8).repeat(32, 0).repeat(32, 1)
+            img = np.clip(base.astype(np.int16) + rng.integers(-6, 7, (H, W, 3)), 0, 255).astype(np.uint8)
+            lab = rng.integers(0, 34, (H // 32, W // 32), dtype=np.uint8).repeat(32, 0).repeat(32, 1)
+            recs.append(encode_example({
+                'image/encoded': [encode_png(img)], 'image/format': [b'png'],
+                'image/shape': [H, W, 3], 'image/path': [f'img_{i}.png'.encode()],
+                'label/encoded': [encode_png(lab[..., None])], 'label/format': [b'png'],
+                'label/shape': [H, W, 1], 'label/path': [f'lab_{i}.png'.encode()]}))
+        path = os.path.join(tmp, "cityscapes_1024x2048.tfrecord")
+        write_records(path, recs)
+        png_mb = sum(len(r) for r in recs) / len(recs) / 1e6
+        t_gen = time.perf_counter() - t_gen
+        out = {"decode_workers": default_workers(), "prefetch_batches": 2, "steps": steps,
+               "warmup": warmup, "record_mb": round(png_mb, 2)}
+        pyr = {"aspp": ["--aspp_module"], "psp": ["--psp_module"], "none": []}[args.pyramid]
+        for mode in ("real_data", "synthetic"):
+            mh.release_contexts()
+            get_or_create_global_step().value = 0
+            argv = [os.path.join(tmp, mode), "cityscapes", "--max_steps", str(warmup + steps),
+                    "--compute_dtype", args.dtype, "--height_feature_extractor", str(H),
+                    "--width_feature_extractor", str(W), "--Nb_per_pixel", str(NB),
+                    "--Nb_per_bbox", "0", "--Nb_per_image", "0",
+                    "--save_summaries_steps", "1000000", "--save_checkpoints_steps", "1000000"] + pyr
+            if mode == "real_data":
+                argv += ["--tfrecords_path_per_pixel", path]
+            else:   # the resident pool fills during the warm-up steps (host generation)
+                argv += ["--synthetic_pool", str(warmup)]
+            system, _ = train.build_system(argv)
+            system.train(max_steps=warmup + steps, log_fn=lambda *a: None, timing_warmup=warmup)
+            tm = system.last_train_timing
+            out[mode] = {"images_per_sec": round(tm["images"] / tm["seconds"], 3),
+                         "ms_per_step": round(tm["seconds"] * 1e3 / tm["steps"], 2)}
+            mh.release_contexts()
+        out["images_per_sec"] = out["real_data"]["images_per_sec"]
+        out["what"] = (f"train.py (SemanticSegmentation.train) on the bench workload, {NB} images/step; "
+                       f"real_data: {len(recs)} generated 1024x2048 PNG TFRecords ({png_mb:.1f} MB "
+                       f"each, written in {t_gen:.0f} s), host decode on {out['decode_workers']} "
+                       "threads 2 batches ahead; synthetic: seeded batches resident in HBM")
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,6 +221,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--no-train-py", action="store_true",
+                    help="skip the drop-in trainer leg (train.py on real and synthetic data)")
     ap.add_argument("--no-defer-stem", action="store_true",
                     help="A/B: join every weight gradient before the update (the N > 1 order)")
     args = ap.parse_args()
@@ -207,12 +278,14 @@ def main():
 
     from estimator.define_estimator_hierarchical import ema_decay_effective
     gstep = [0]
+    comm_ev = []      # (backward issued, last all-reduce done) per timed step, N > 1
+    timing = [None]
 
     def step():
         ctx.forward(img)
         ctx.loss(px, bbox, tag)
         ctx.backward()
-        scale = allreduce_grads(ctx)
+        scale = allreduce_grads(ctx, timing=timing[0])
         ema = ema_decay_effective(EMA_DECAY, gstep[0]) if ema_on else 0.0
         ctx.apply_update(0.01, 0.9, ema, scale)
         gstep[0] += 1
@@ -237,6 +310,8 @@ def main():
         dist.barrier()
     # HIP-event kernel timing (roofline) is recorded on the launch stream during the LAST timed
     # step only: events around every conv launch of every step cost ~1.8 ms per step
+    if world > 1:
+        timing[0] = comm_ev
     t0 = time.perf_counter()
     for i in range(args.steps):
         if i == args.steps - 1 and not args.no_profile:
@@ -246,10 +321,26 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    timing[0] = None
+    comm = {"world_size": world, "backend": None, "allreduce_bytes_per_step": None,
+            "buckets": None, "exposed_allreduce_ms": None, "exposed_allreduce_ms_max_rank": None}
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # what the process group saw and what the gradient exchange cost: bytes all-reduced per
+        # step (fp32 [grads | BN statistics]), and the all-reduce time the update waited for
+        # after this rank's backward had been issued (mean over the timed steps; the max over
+        # ranks beside it)
+        bk = ctx.grad_buckets()
+        exposed = [max(0.0, a.elapsed_time(b)) for a, b in comm_ev]
+        ex = sum(exposed) / max(len(exposed), 1)
+        te = torch.tensor([ex], device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        comm.update(world_size=dist.get_world_size(), backend=str(dist.get_backend()),
+                    allreduce_bytes_per_step=int(sum(hi - lo for lo, hi in bk) * 4),
+                    buckets=len(bk), exposed_allreduce_ms=round(ex, 3),
+                    exposed_allreduce_ms_max_rank=round(float(te.item()), 3))
     losses, _, _ = ctx.outputs()
     lv = losses.cpu().numpy()
     if not np.all(np.isfinite(lv)):
@@ -278,8 +369,9 @@ def main():
         achieved = r["gflop"] / r["ms"]  # GFLOP/ms == TFLOP/s
         # HBM bytes per launch of that class from the committed PMC passes of this code
         # (tools/pmc_traffic.sh + tools/pmc_traffic.py; rocprofv3 cannot run inside the bench)
-        traffic, tsrc = None, None
-        for tname in ("r03_pmc_traffic.json", "r02_pmc_traffic.json", "r01_pmc_traffic.json"):
+        traffic, tsrc, step_ledger = None, None, None
+        for tname in ("r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json",
+                      "r01_pmc_traffic.json"):
             tpath = os.path.join(REPO, "profiles", tname)
             if not os.path.exists(tpath):
                 continue
@@ -288,6 +380,8 @@ def main():
             if key in tj:
                 traffic = round(tj[key]["hbm_bytes_per_launch"])
                 tsrc = f"profiles/{tname} ({key}, bytes per launch)"
+                if "hbm_bytes" in tj.get("step", {}):
+                    step_ledger = (tj["step"], f"profiles/{tname} (step)")
                 break
         # the north star's named target: the dilated 3x3 convs of the encoder (block3 rate 2,
         # block4 rate 4, and the ASPP rates), per pass, against the MFMA peak
@@ -325,6 +419,18 @@ def main():
             if nm in all_classes and all_classes[nm]["ms"] > 0:
                 all_classes[nm]["attainable_frac"] = round(b_ms / all_classes[nm]["ms"], 4)
         step_bound = round(sum(bound_ms.values()) / (elapsed * 1e3 / args.steps), 4)
+        # the whole step against the chip: algorithmic conv flops at the MFMA peak vs the HBM-side
+        # bytes of one step (PMC ledger, every kernel) at the achievable 6.29 TB/s
+        # (MI355X_MICROARCH.md): the larger is the step's floor
+        step_ms = elapsed * 1e3 / args.steps
+        step_tflop = sum(row["gflop"] for row in dump if row["cls"] <= 2) / 1e3
+        step_roof = {"tflop": round(step_tflop, 3), "mfma_ms": round(step_tflop / peak * 1e3, 3)}
+        if step_ledger:
+            sb = step_ledger[0]["hbm_bytes"]
+            step_roof.update(hbm_bytes=round(sb), hbm_ms=round(sb / 6.29e12 * 1e3, 3),
+                             source=step_ledger[1])
+            step_roof["bound_ms"] = max(step_roof["mfma_ms"], step_roof["hbm_ms"])
+            step_roof["frac"] = round(step_roof["bound_ms"] / step_ms, 4)
         names = dict(CLS_NAMES, **(CLS_NAMES_F32 if args.dtype == "fp32" else {}))
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -345,6 +451,8 @@ def main():
                     "dilated_3x3_encoder": dilated,
                     "attainable_frac": all_classes.get(CLS_NAMES[dom], {}).get("attainable_frac"),
                     "step_bound_frac": step_bound,
+                    "step_hbm_bytes": step_roof.get("hbm_bytes"),
+                    "step": step_roof,
                     "max_layer": r["max_layer"]}
         ctx.profile(False)
 
@@ -388,6 +496,11 @@ def main():
         ev = {"images_per_sec_per_gpu": round(NB / te, 3), "ms_per_batch": round(te * 1e3, 2),
               "batch": NB, "miou_eval": round(float(emiou), 3),
               "what": "moving-statistics BN forward + seg_predict + confusion (3 batches)"}
+    ctx.close()
+    train_py = None
+    if world == 1 and not args.no_train_py and args.config == "C2":
+        train_py = train_py_leg(args)
+        train_py["ratio_to_value"] = round(train_py["images_per_sec"] / (NB * args.steps / elapsed), 3)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C2":
         cpu = cpu_baseline(pyramid=args.pyramid)
@@ -413,9 +526,10 @@ def main():
                "loss_scale": None if scaler is None else {
                    "scale": scaler.scale, "skipped_warmup": skipped0, "calibration_steps": calib,
                    "skipped_timed": scaler.skipped - skipped0},
+               "comm": comm,
+               "train_py": train_py,
                "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
-    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

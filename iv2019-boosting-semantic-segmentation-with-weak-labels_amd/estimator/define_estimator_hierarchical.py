@@ -44,7 +44,7 @@ def world_size():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
-def allreduce_grads(ctx, overlap=True, always=False):
+def allreduce_grads(ctx, overlap=True, always=False, timing=None):
     """SUM all-reduce of the flat gradient buffer (gradients + BN batch-statistics tail) over
     the process group (RCCL over xGMI on MI355X; gloo on CPU tests). Returns the scale that
     turns the sum into the tower mean (applied inside the fused update).
@@ -54,7 +54,12 @@ def allreduce_grads(ctx, overlap=True, always=False):
     collective waiting only for its bucket's event, so the all-reduce of the head and upper
     layers overlaps the backward of the lower ones; the compute stream waits for the side
     stream before the update. `always` runs the collective even in a one-rank group (tests
-    of the RCCL path on one GPU); otherwise a single rank skips it."""
+    of the RCCL path on one GPU); otherwise a single rank skips it.
+
+    `timing` (a list, GPU bucketed path only): appends (backward_done, comm_done) events --
+    recorded on the compute stream when its backward has been issued, and on the comm stream
+    after the last bucket's collective -- so backward_done.elapsed_time(comm_done), when
+    positive, is the all-reduce time the update waits for (exposed, not overlapped)."""
     import torch
     import torch.distributed as dist
     n = world_size()
@@ -66,10 +71,16 @@ def allreduce_grads(ctx, overlap=True, always=False):
         comm = getattr(ctx, '_comm_stream', None)
         if comm is None:
             comm = ctx._comm_stream = torch.cuda.Stream(ctx.grads.device)
+        if timing is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record(main)
         for i, (lo, hi) in enumerate(buckets):
             ctx.wait_bucket(i, comm)
             with torch.cuda.stream(comm):
                 dist.all_reduce(ctx.grads[lo:hi], op=dist.ReduceOp.SUM)
+        if timing is not None:
+            ev1.record(comm)
+            timing.append((ev0, ev1))
         main.wait_stream(comm)
     elif buckets:
         for lo, hi in buckets:   # host buffers (gloo): the same bucket order, no streams

@@ -98,7 +98,14 @@ class SemanticSegmentation(object):
         if not s.save_checkpoints_steps:
             s.save_checkpoints_steps = s.num_batches_per_epoch
 
-    def train(self, max_steps=None, log_fn=print):
+    def train(self, max_steps=None, log_fn=print, timing_warmup=None):
+        """The training loop (system_factory.py:189-302). `timing_warmup` = w: after the w-th
+        step of this call the device is synchronised and a clock starts; it stops after a final
+        synchronisation, and ``self.last_train_timing`` = {'steps', 'seconds', 'images'} of the
+        steps in between (throughput of the whole drop-in path, input pipeline included)."""
+        return self._train(max_steps, log_fn, timing_warmup)
+
+    def _train(self, max_steps, log_fn, timing_warmup):
         import torch
         s = self._settings
         self._prepare_train_settings()
@@ -132,7 +139,12 @@ class SemanticSegmentation(object):
         if rank == 0:
             log_fn(f"training {total} steps on {n} GPU(s)")
         t0 = time.time()
+        first, t_timed = step.value, None
+        self.last_train_timing = None
         while step.value < total:
+            if timing_warmup is not None and step.value - first == timing_warmup:
+                torch.cuda.synchronize()
+                t_timed, s_timed = time.perf_counter(), step.value
             features, labels = next(data)
             spec = self._estimator_fn(ModeKeys.TRAIN, features, labels, config=config, params=s)
             ctx = spec.predictions['_context']
@@ -146,6 +158,11 @@ class SemanticSegmentation(object):
                        f"({(time.time() - t0) / max(step.value, 1):.3f} s/step)")
             if rank == 0 and step.value % s.save_checkpoints_steps == 0:
                 self.save(ctx, step.value)
+        if t_timed is not None:
+            torch.cuda.synchronize()
+            n = step.value - s_timed
+            self.last_train_timing = {'steps': n, 'seconds': time.perf_counter() - t_timed,
+                                      'images': n * int(features['proimages'].shape[0])}
         if rank == 0 and ctx is not None:
             self.save(ctx, step.value)
         return step.value

@@ -26,23 +26,44 @@ from system_factory import SemanticSegmentation  # noqa: E402
 from utils.utils import SemanticSegmentationArguments  # noqa: E402
 
 
+def rank_sub_batches(config, params):
+    """This rank's share of every sub-batch: get_temp_Nb (input_pipelines/utils.py:118-125)
+    applied to the per-pixel, per-bbox and per-image streams separately, as the reference's
+    per-tower input does (per_pixel_per_bbox_per_image.py:20-87 under MirroredStrategy)."""
+    return [get_temp_Nb(config, params.Nb_per_pixel), get_temp_Nb(config, params.Nb_per_bbox),
+            get_temp_Nb(config, params.Nb_per_image)]
+
+
+def synthetic_seed(rank, step):
+    return 1000003 * rank + step
+
+
 def synthetic_train_input(config, params):
-    """Endless seeded batches shaped like the heterogeneous-supervision pipeline, per rank."""
+    """Endless seeded batches shaped like the heterogeneous-supervision pipeline, per rank.
+
+    The first ``--synthetic_pool`` batches (seeds synthetic_seed(rank, k)) are generated on
+    the host once and stay resident in HBM; later steps cycle through them. Regenerating
+    every step would cost the host ~0.1 GB of images + 126 MB of soft labels per weak image
+    at 1024 x 2048 plus the H2D copies, far more than the device step."""
     import torch
     from input_pipelines.synthetic import batch
     rank = int(os.environ.get('RANK', 0))
-    nb = [get_temp_Nb(config, params.Nb_per_pixel), get_temp_Nb(config, params.Nb_per_bbox),
-          get_temp_Nb(config, params.Nb_per_image)]
+    nb = rank_sub_batches(config, params)
     dev = torch.device('cuda', torch.cuda.current_device())
+    pool_n = max(1, int(getattr(params, 'synthetic_pool', 8) or 1))
+    pool = []
     step = 0
     while True:
-        b = batch(1000003 * rank + step, *nb, params.height_feature_extractor,
-                  params.width_feature_extractor)
-        feats = {'proimages': torch.as_tensor(b['images']).to(dev)}
-        labels = {'prolabels_per_pixel': torch.as_tensor(b['px']).to(dev),
-                  'prolabels_per_bbox': torch.as_tensor(b['bbox']).to(dev) if nb[1] else None,
-                  'prolabels_per_image': torch.as_tensor(b['tag']).to(dev) if nb[2] else None}
-        yield feats, labels
+        if len(pool) < pool_n:
+            b = batch(synthetic_seed(rank, step), *nb, params.height_feature_extractor,
+                      params.width_feature_extractor)
+            pin = lambda a: torch.from_numpy(a).pin_memory().to(dev, non_blocking=True)
+            pool.append(({'proimages': pin(b['images'])},
+                         {'prolabels_per_pixel': pin(b['px']),
+                          'prolabels_per_bbox': pin(b['bbox']) if nb[1] else None,
+                          'prolabels_per_image': pin(b['tag']) if nb[2] else None}))
+            del b
+        yield pool[step % pool_n]
         step += 1
 
 
@@ -57,6 +78,13 @@ def add_train_input_pipeline_arguments(argparser):
     argparser.add_argument('--bboxes_images_dir', type=str, default=None)
     argparser.add_argument('--image_labels_index_path', type=str, default=None)
     argparser.add_argument('--image_labels_images_dir', type=str, default=None)
+    argparser.add_argument('--input_workers', type=int, default=0,
+                           help='real-data decode threads (0: NUM_PARALLEL_CALLS = 15, capped '
+                                'at the usable cores)')
+    argparser.add_argument('--input_prefetch', type=int, default=2,
+                           help='real-data batches decoded ahead of the training step')
+    argparser.add_argument('--synthetic_pool', type=int, default=8,
+                           help='synthetic input: seeded batches kept resident in HBM and cycled')
     argparser.add_argument('--input_seed', type=int, default=0,
                            help='seed of the shuffles and crop offsets (the reference seeds nothing)')
 
@@ -85,13 +113,18 @@ def _add_extra_args(settings):
     settings.preserve_aspect_ratio_per_image = True
 
 
-def main(argv):
+def build_system(argv):
+    """train.py's settings and facade, without running it: (system, settings)."""
     ssargs = SemanticSegmentationArguments(mode=ModeKeys.TRAIN)
     add_train_input_pipeline_arguments(ssargs.argparser)
     add_model_arguments(ssargs.argparser)
     settings = ssargs.parse_args(argv)
     _add_extra_args(settings)
-    system = SemanticSegmentation({'train': train_input_fn(settings)}, model_fn, settings)
+    return SemanticSegmentation({'train': train_input_fn(settings)}, model_fn, settings), settings
+
+
+def main(argv):
+    system, settings = build_system(argv)
     return system.train(max_steps=settings.max_steps)
 
 

@@ -162,3 +162,153 @@ def test_cross_replica_bn_two_ranks_matches_oracle():
     for k, v in newp.items():
         if "moving" in k:
             assert rel(res[0][3][k], v.detach().numpy()) < 1e-3, k
+
+
+DP4_H, DP4_W, DP4_WORLD = 64, 128, 4
+
+
+def _dp4_worker(rank, port, tmp, q):
+    """One rank of `train.py --distribute` at world size 4 (gloo over CUDA tensors: one GPU
+    cannot host four RCCL ranks) with the reference's global 4 : 8 : 4 pixel : bbox : tag batch
+    (train.py:62-64), one fp32 step at 64 x 128: records this rank's sub-batch, loss terms and
+    counts, weak l1 decisions, and the state after the update."""
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                          WORLD_SIZE=str(DP4_WORLD), RANK=str(rank), LOCAL_RANK="0")
+        dist.init_process_group("gloo", rank=rank, world_size=DP4_WORLD)
+        import train
+        import estimator.define_estimator_hierarchical as deh
+        from models import resnet50_extended_model_hierarchical as mh
+        seen = []
+        orig = deh.define_losses
+
+        def wrapped(mode, predictions, labels, config, params):
+            L = orig(mode, predictions, labels, config, params)
+            ctx = predictions['_context']
+            lv = ctx.outputs()[0].cpu().numpy()[:4].copy()
+            d1 = predictions['l1_decisions'][ctx.cfg.nb_pp:].cpu().numpy().astype(np.int64)
+            seen.append(((ctx.cfg.nb_pp, ctx.cfg.nb_pb, ctx.cfg.nb_pi), lv, L.counts(), d1,
+                         int(config.train_distribute.num_towers)))
+            return L
+        deh.define_losses = wrapped
+        argv = [os.path.join(tmp, "logs"), "cityscapes", "--max_steps", "1", "--compute_dtype", "fp32",
+                "--height_feature_extractor", str(DP4_H), "--width_feature_extractor", str(DP4_W),
+                "--Nb_per_pixel", "4", "--Nb_per_bbox", "8", "--Nb_per_image", "4",
+                "--learning_rate_initial", "1e-3", "--save_summaries_steps", "1",
+                "--save_checkpoints_steps", "100", "--distribute"]
+        assert train.main(argv) == 1
+        ctx = next(iter(mh._CONTEXTS.values()))
+        torch.cuda.synchronize()
+        tail = ctx.grads[ctx.n_train:].cpu().numpy().copy()   # averaged BN batch statistics
+        q.put((rank, seen, ctx.named("params"), tail, None))
+        mh.release_contexts()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        q.put((rank, None, None, None, traceback.format_exc() + repr(e)))
+
+
+def test_four_ranks_mixed_batch_matches_oracle(tmp_path):
+    """MirroredStrategy semantics at world size 4 with the reference's
+    mixed batch, through the drop-in trainer. Each rank must take Nb/4 of EVERY sub-batch
+    (get_temp_Nb per stream, input_pipelines/utils.py:118-125: 1 strong + 2 bbox + 1 tag),
+    normalise its losses by its own non-zero-weight counts (define_losses per tower), and
+    the step must apply the MEAN of the four per-rank gradients and of the four per-rank BN
+    batch statistics (the moving averages' input). Checked against the oracle run with the
+    identical sharding: each rank's shard through OracleNet (same seeds as
+    train.synthetic_train_input, same weak-weight mask as the native rank), then the mean.
+    Tolerances: per-rank losses 1e-3 and counts exact; the parameter change and the averaged
+    statistics tail L2-relative max(1e-2, 3x) / max(1e-3, 4x) the fp32 oracle's own gap."""
+    import torch
+    import torch.multiprocessing as mp
+    from input_pipelines.synthetic import batch
+    from oracle.tfseg import OracleNet, SegConfig, init_params
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    port = _free_port()
+    procs = [mctx.Process(target=_dp4_worker, args=(r, port, str(tmp_path / f"r{r}"), q))
+             for r in range(DP4_WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[4] is None, r[4]
+    for rank, seen, _, _, _ in res:
+        assert len(seen) == 1 and seen[0][0] == (1, 2, 1) and seen[0][4] == DP4_WORLD, (rank, seen)
+    # every rank applied the same averaged update
+    for k in res[0][2]:
+        for r in range(1, DP4_WORLD):
+            np.testing.assert_array_equal(res[0][2][k], res[r][2][k])
+    np.testing.assert_array_equal(res[0][3], res[1][3])
+
+    cfg = SegConfig(height=DP4_H, width=DP4_W, nb_pp=1, nb_pb=2, nb_pi=1, pyramid="none")
+    p0 = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=0).items()}
+
+    def oracle(dtype):
+        losses, counts, grads, stats = [], [], [], []
+        for r in range(DP4_WORLD):
+            d = batch(1000003 * r, 1, 2, 1, DP4_H, DP4_W)   # train.synthetic_train_input, rank r
+            net = OracleNet(cfg, {k: v.astype(np.float64) for k, v in p0.items()}, dtype=dtype)
+            L, _, g, _, _, _, st = net.train_step(d["images"], d["px"], d["bbox"], d["tag"],
+                                                  lr=1e-3, weak_l1_decisions=res[r][1][0][3])
+            losses.append([float(L[n]) for n in ("segmentation", "l1_segmentation",
+                                                  "l2_vehicle_segmentation", "l2_human_segmentation")])
+            counts.append(tuple(int(c) for c in L["counts"]))
+            grads.append({k: v.detach().numpy() for k, v in g.items()})
+            stats.append({k: (m.detach().numpy(), v.detach().numpy()) for k, (m, v) in st.items()})
+        g = {k: sum(gr[k] for gr in grads) / DP4_WORLD for k in grads[0]}
+        st = {k: (sum(s[k][0] for s in stats) / DP4_WORLD, sum(s[k][1] for s in stats) / DP4_WORLD)
+              for k in stats[0]}
+        # step 0 of MomentumOptimizer: accum = g + wd * w; w -= lr * accum
+        new_p = {k: p0[k] - 1e-3 * (g[k] + (cfg.weight_decay * p0[k] if k.endswith("/weights") else 0.0))
+                 for k in g}
+        return losses, counts, new_p, st
+
+    ref_l, ref_c, ref_p, ref_s = oracle(torch.float64)
+    _, _, p32, s32 = oracle(torch.float32)
+    for r in range(DP4_WORLD):
+        np.testing.assert_allclose(res[r][1][0][1], ref_l[r], rtol=1e-3, atol=1e-6, err_msg=f"rank {r}")
+        assert tuple(res[r][1][0][2]) == ref_c[r], (r, res[r][1][0][2], ref_c[r])
+    # per-rank normalisation is not the global one: the ranks' counts differ
+    assert len(set(ref_c)) > 1
+
+    def rel(a, b):
+        a, b = np.asarray(a, np.float64).reshape(-1), np.asarray(b, np.float64).reshape(-1)
+        return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+    keys = sorted(ref_p)
+    flat = lambda d: np.concatenate([np.asarray(d[k], np.float64).reshape(-1) for k in keys])
+    w0 = flat(p0)
+    err = rel(flat(res[0][2]) - w0, flat(ref_p) - w0)
+    gap = rel(flat(p32) - w0, flat(ref_p) - w0)
+    assert err < max(1e-2, 3 * gap), (err, gap)
+    # the statistics tail (moving-buffer layout): rank-mean of the batch means / variances
+    info = {}
+    for k, (m, v) in ref_s.items():
+        info[f"{k}/BatchNorm/moving_mean"] = m
+        info[f"{k}/BatchNorm/moving_variance"] = v
+    info32 = {}
+    for k, (m, v) in s32.items():
+        info32[f"{k}/BatchNorm/moving_mean"] = m
+        info32[f"{k}/BatchNorm/moving_variance"] = v
+    tail = res[0][3]
+    offs = _moving_offsets(cfg)
+    got = np.concatenate([tail[offs[k][0]:offs[k][0] + offs[k][1]] for k in sorted(info)])
+    exp = np.concatenate([np.asarray(info[k]).reshape(-1) for k in sorted(info)])
+    e32 = np.concatenate([np.asarray(info32[k]).reshape(-1) for k in sorted(info)])
+    assert rel(got, exp) < max(1e-3, 4 * rel(e32, exp)), (rel(got, exp), rel(e32, exp))
+
+
+def _moving_offsets(cfg):
+    """name -> (offset, numel) of the moving statistics in the context's moving buffer (the
+    layout of the gradient buffer's statistics tail), from a throw-away context."""
+    from seg_hip import SegContext
+    ctx = SegContext(pyramid="none", height=cfg.height, width=cfg.width, nb_pp=cfg.nb_pp,
+                     nb_pb=cfg.nb_pb, nb_pi=cfg.nb_pi, dtype="fp32")
+    out = {p.name: (p.offset, p.numel) for p in ctx.param_info
+           if p.kind in ("moving_mean", "moving_variance")}
+    ctx.close()
+    return out

@@ -166,3 +166,83 @@ def test_initializer_matches_oracle_scheme():
     ref = oracle_init(cfg, seed=7)
     for k in ours:
         np.testing.assert_allclose(ours[k].reshape(-1), ref[k].reshape(-1).astype(np.float32))
+
+
+DP4 = dict(H=32, W=64, world=4)
+
+
+def _dp4_cpu_worker(rank, port, q):
+    """One rank of a world-size-4 data-parallel step on the CPU (gloo): this rank's share of
+    the reference's 4 : 8 : 4 batch (train.rank_sub_batches under DistributeConfig(4), seeds
+    of train.synthetic_seed), the oracle standing in for the device engine, and the host
+    gradient exchange of the product (allreduce_grads over a flat [grads | BN-stat tail]
+    buffer, bucket by bucket)."""
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.set_num_threads(2)
+        dist.init_process_group("gloo", rank=rank, world_size=DP4["world"])
+        import train
+        from estimator.define_estimator_hierarchical import allreduce_grads
+        from input_pipelines.synthetic import batch
+        from oracle.tfseg import OracleNet, SegConfig, init_params
+        from system_factory import DistributeConfig
+        from types import SimpleNamespace
+        config = SimpleNamespace(train_distribute=DistributeConfig(DP4["world"]))
+        params = SimpleNamespace(Nb_per_pixel=4, Nb_per_bbox=8, Nb_per_image=4)
+        nb = train.rank_sub_batches(config, params)
+        cfg = SegConfig(height=DP4["H"], width=DP4["W"], nb_pp=nb[0], nb_pb=nb[1], nb_pi=nb[2],
+                        pyramid="none")
+        d = batch(train.synthetic_seed(rank, 0), *nb, DP4["H"], DP4["W"])
+        net = OracleNet(cfg, init_params(cfg, seed=0))
+        L, _, g, _, _, _, st = net.train_step(d["images"], d["px"], d["bbox"], d["tag"])
+        keys = sorted(g)
+        skeys = sorted(st)
+        flat = torch.cat([g[k].reshape(-1) for k in keys] +
+                         [torch.cat([st[k][0].reshape(-1), st[k][1].reshape(-1)]) for k in skeys]).float()
+        n_g = sum(g[k].numel() for k in keys)
+
+        class Ctx:   # the bound flat buffer and the backward's bucket order (tail last)
+            grads = flat.clone()
+
+            @staticmethod
+            def grad_buckets():
+                return [(n_g // 2, n_g), (0, n_g // 2), (n_g, flat.numel())]
+        scale = allreduce_grads(Ctx)
+        q.put((rank, nb, float(L["segmentation"]), tuple(int(c) for c in L["counts"]),
+               flat.numpy(), (Ctx.grads * scale).numpy(), None))
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        q.put((rank, None, None, None, None, None, traceback.format_exc() + repr(e)))
+
+
+def test_dp_four_ranks_mixed_batch_host_path():
+    """VERDICT r3 item 5 on the CPU: at world size 4 each rank takes a quarter of EVERY
+    sub-batch (1 strong + 2 bbox + 1 tag of the reference's 4 : 8 : 4, get_temp_Nb per
+    stream), normalises its loss by its own non-zero-weight counts (they differ between the
+    ranks, so a global normalisation would give other gradients), and the bucketed SUM
+    all-reduce scaled by 1/4 yields, on every rank, exactly the mean of the four per-rank
+    [gradients | BN batch statistics] buffers (fp32 sums of 4 values: within a few ulp of
+    the sum of their magnitudes)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp4_cpu_worker, args=(r, port, q)) for r in range(DP4["world"])]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[6] is None, r[6]
+    assert all(r[1] == [1, 2, 1] for r in res)
+    assert len({r[3] for r in res}) > 1          # per-rank counts differ
+    local = np.stack([r[4] for r in res]).astype(np.float64)
+    mean = local.mean(0)
+    bound = 4 * np.finfo(np.float32).eps * np.abs(local).sum(0) / 4 + 1e-30
+    for r in res:
+        assert np.all(np.abs(r[5] - mean) <= bound), float(np.max(np.abs(r[5] - mean) / bound))
+        np.testing.assert_array_equal(r[5], res[0][5])
