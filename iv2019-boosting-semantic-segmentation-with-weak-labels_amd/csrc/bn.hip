@@ -479,7 +479,7 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
   Raw8<TZ> rdz[BN_U], rz[BN_U];
   Raw8<T> ry[BN_U];
   uint32_t mk[BN_U];
-  const int cg = c0 >> 3, cgn = a.C >> 3;
+  const int cg = c0 >> 3, cgn = a.ldm ? a.ldm : a.C >> 3;
 #pragma unroll
   for (int k = 0; k < BN_U; ++k) {
     if (FULL || k < nrows) {
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_dual_kernel(BnBwdArgs a) {
     const T* DZ = (const T*)a.dz + c0;
     const T* Y = (const T*)a.y + c0;
     const T* Y2 = (const T*)a.y2 + c0;
-    const int cg = c0 >> 3, cgn = a.C >> 3;
+    const int cg = c0 >> 3, cgn = a.ldm ? a.ldm : a.C >> 3;
     for (long base = r0 + L.rl; base < r1; base += (long)L.rpp * U) {
       Raw8<T> rdz[U], ry[U], ry2[U];
       uint32_t mk[U];
@@ -716,7 +716,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_dual_kernel(BnBwdArgs a) {
   const T* Y2 = (const T*)a.y2 + c0;
   T* DY = (T*)a.dy + c0;
   T* DY2 = (T*)a.dy2 + c0;
-  const int cg = c0 >> 3, cgn = a.C >> 3;
+  const int cg = c0 >> 3, cgn = a.ldm ? a.ldm : a.C >> 3;
   const long step = (long)L.rpp * U;
   for (long base = (long)blockIdx.x * step + L.rl; base < a.M; base += (long)gridDim.x * step) {
     Raw8<T> rdz[U], ry[U], ry2[U];

@@ -462,6 +462,10 @@ WgradArgs wgrad_problem(const ConvL& L, bool s2d) {
   return a;
 }
 
+#ifndef SEG_BN_SLAB_MB
+#define SEG_BN_SLAB_MB 0   // BN-backward channel slabs (bn_backward); 0 = whole layers
+#endif
+
 // ------------------------------------------------------------------------------------------
 // kernel sequencing helpers
 // ------------------------------------------------------------------------------------------
@@ -619,29 +623,58 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   a.part = L.bwd_part; a.rb = L.rb;
   a.dzscale = dzscale;
   const double esz = seg_half(S.dt) ? 2.0 : 4.0, zsz = dz_f32 ? 4.0 : esz;
-  const double me = a.M * (double)a.C * 1e-9;
-  const double gb_in = me * (zsz + (a.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
-  int slot;
-  if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
-  HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
-  if (int r = prof_end(c, S.s, slot)) return r;
   const bool tb = c->cfg.train_bn != 0;
-  // a backward after a moving-statistics forward (TRAIN without
-  // batch_norm_accumulate_statistics) differentiates through constant statistics
-  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
-                                    tb ? c->grads + L.g_off : nullptr,
-                                    tb ? c->grads + L.b_off : nullptr, S.s, c->bn_infer));
-  if (c->sync_fn && !c->bn_infer) {
-    // [mean(dyhat) | mean(dyhat * xhat)] (contiguous in the layer's state) averaged over the
-    // replicas: dx is the gradient through the global statistics; dgamma / dbeta stay this
-    // replica's sums (the gradient all-reduce averages them)
-    if (int r = sync_exchange(c, L.st.sdy, 2L * L.co, S.s)) return r;
-    HIPCALL(c, launch_scale2(L.st.sdy, 2L * L.co, 1.f / c->sync_world, 0, 1.f, S.s));
+  // channel slabs (SEG_BN_SLAB_MB): reduce -> finalize -> apply per slab of channels whose
+  // dz + y bytes fit the Infinity Cache, so the apply's re-read of them is served on-die
+  int cs = a.C;
+  const double row_b = (zsz + esz) * (double)a.M;
+  if (SEG_BN_SLAB_MB > 0 && !c->sync_fn && !dz_f32 && a.C % 64 == 0 &&
+      row_b * a.C > SEG_BN_SLAB_MB * 1048576.0) {
+    cs = (int)(SEG_BN_SLAB_MB * 1048576.0 / row_b) / 64 * 64;
+    if (cs < 64) cs = 64;
+    while (a.C % cs) cs -= 64;   // equal slabs
   }
-  const double gb_apply = gb_in + me * esz * (dyhat_out ? 2 : 1);
-  if (int r = prof_begin(c, S.s, 5, li, gb_apply, &slot)) return r;
-  HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
-  return prof_end(c, S.s, slot);
+  if (a.mask && cs < a.C) a.ldm = a.C / 8;
+  for (int c0 = 0; c0 < a.C; c0 += cs) {
+    BnBwdArgs b = a;
+    BnState st = L.st;
+    if (cs < a.C) {
+      const size_t eo = (size_t)c0 * (size_t)(dz_f32 ? 4 : c->esz), ey = (size_t)c0 * c->esz;
+      b.dz = (const char*)a.dz + eo;
+      if (a.z) b.z = (const char*)a.z + eo;
+      if (a.mask) b.mask = a.mask + c0 / 8;
+      b.y = (const char*)a.y + ey;
+      b.dy = (char*)a.dy + ey;
+      if (a.dyhat) b.dyhat = (char*)a.dyhat + ey;
+      if (a.dzscale) b.dzscale = a.dzscale + c0;
+      b.C = cs;
+      st.mean += c0; st.invstd += c0; st.scale += c0; st.var_unb += c0; st.sdy += c0; st.sdyx += c0;
+      b.mean = st.mean; b.invstd = st.invstd; b.scale = st.scale; b.sdy = st.sdy; b.sdyx = st.sdyx;
+    }
+    const double me = b.M * (double)b.C * 1e-9;
+    const double gb_in = me * (zsz + (b.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
+    int slot;
+    if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
+    HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, b, S.s));
+    if (int r = prof_end(c, S.s, slot)) return r;
+    // a backward after a moving-statistics forward (TRAIN without
+    // batch_norm_accumulate_statistics) differentiates through constant statistics
+    HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, b.M, b.C, st,
+                                      tb ? c->grads + L.g_off + c0 : nullptr,
+                                      tb ? c->grads + L.b_off + c0 : nullptr, S.s, c->bn_infer));
+    if (c->sync_fn && !c->bn_infer) {
+      // [mean(dyhat) | mean(dyhat * xhat)] (contiguous in the layer's state) averaged over the
+      // replicas: dx is the gradient through the global statistics; dgamma / dbeta stay this
+      // replica's sums (the gradient all-reduce averages them)
+      if (int r = sync_exchange(c, L.st.sdy, 2L * L.co, S.s)) return r;
+      HIPCALL(c, launch_scale2(L.st.sdy, 2L * L.co, 1.f / c->sync_world, 0, 1.f, S.s));
+    }
+    const double gb_apply = gb_in + me * esz * (dyhat_out ? 2 : 1);
+    if (int r = prof_begin(c, S.s, 5, li, gb_apply, &slot)) return r;
+    HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, b, S.s));
+    if (int r = prof_end(c, S.s, slot)) return r;
+  }
+  return 0;
 }
 
 // BN backward of two layers gated by the same dz / ReLU bits (a projection unit's conv3 and

@@ -27,6 +27,7 @@ def cls(n):
 def step_rows(db):
     c = sqlite3.connect(db)
     rows = c.execute("select name, stream_id, start, end from kernels order by start").fetchall()
+    rows = [r for r in rows if "at::native" not in r[0]]   # host-side torch ops (train.py loss sums)
     starts = [r[2] for r in rows if "cast_s2d_kernel" in r[0] or "cast_pad8_kernel" in r[0]]
     t0, t1 = starts[-3], starts[-2]
     step = [r for r in rows if t0 <= r[2] < t1]
