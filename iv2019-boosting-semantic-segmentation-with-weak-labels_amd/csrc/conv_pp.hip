@@ -517,13 +517,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     auto pack4 = [](const f32x4_t& v) {
       u32x2_t w;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const E lo = TypeOps<E>::from_f(v[2 * h]), hi = TypeOps<E>::from_f(v[2 * h + 1]);
-        uint16_t bl, bh;
-        __builtin_memcpy(&bl, &lo, 2);
-        __builtin_memcpy(&bh, &hi, 2);
-        w[h] = (uint32_t)bl | ((uint32_t)bh << 16);
-      }
+      for (int h = 0; h < 2; ++h) w[h] = pack2<E>(v[2 * h], v[2 * h + 1]);
       return w;
     };
     char* const stg = smem + BUF;
@@ -583,7 +577,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             float lo = TypeOps<E>::to_f(lo16<E>(x)) + TypeOps<E>::to_f(lo16<E>(r));
             float hi = TypeOps<E>::to_f(hi16<E>(x)) + TypeOps<E>::to_f(hi16<E>(r));
             if (nres == 2) { lo += TypeOps<E>::to_f(lo16<E>(r2)); hi += TypeOps<E>::to_f(hi16<E>(r2)); }
-            v[k][w] = pack4(f32x4_t{lo, hi, 0.f, 0.f})[0];
+            v[k][w] = pack2<E>(lo, hi);
           }
       }
       if (omask) {

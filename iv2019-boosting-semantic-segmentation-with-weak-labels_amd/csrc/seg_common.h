@@ -6,6 +6,7 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <type_traits>
 
 typedef uint16_t bf16_t;  // storage type of bf16 activations/weights
 
@@ -51,6 +52,18 @@ template <> struct TypeOps<f16_t> {
   static __device__ __forceinline__ float to_f(f16_t v) { return (float)v; }
   static __device__ __forceinline__ f16_t from_f(float v) { return (f16_t)v; }   // RNE
 };
+// two values -> one packed 16-bit pair (lo in bits 0-15) by ONE v_cvt_pk_bf16_f32 /
+// v_cvt_pk_f16_f32 (RNE, as the scalar casts): converting the halves separately costs two
+// conversions plus a shift and an SDWA or per pair (the conv epilogues pack 128 values per lane)
+typedef float pk_f32x2_t __attribute__((ext_vector_type(2)));
+template <typename E> __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  typedef __attribute__((ext_vector_type(2))) typename std::conditional<std::is_same<E, f16_t>::value, _Float16, __bf16>::type h2_t;
+  const h2_t r = __builtin_convertvector((pk_f32x2_t){lo, hi}, h2_t);
+  uint32_t u;
+  __builtin_memcpy(&u, &r, 4);
+  return u;
+}
+
 template <typename T> __device__ __forceinline__ float ldf(const T* p) { return TypeOps<T>::to_f(*p); }
 template <typename T> __device__ __forceinline__ void stf(T* p, float v) { *p = TypeOps<T>::from_f(v); }
 
@@ -79,7 +92,7 @@ template <> struct Vec8<bf16_t> {
   static __device__ __forceinline__ void store(bf16_t* p, const float* v) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = pack2<bf16_t>(v[2 * i], v[2 * i + 1]);
     *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
@@ -91,10 +104,10 @@ template <> struct Vec8<f16_t> {
     for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
   }
   static __device__ __forceinline__ void store(f16_t* p, const float* v) {
-    f16x8_t h;
+    uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) h[i] = (f16_t)v[i];
-    *(f16x8_t*)p = h;
+    for (int i = 0; i < 4; ++i) w[i] = pack2<f16_t>(v[2 * i], v[2 * i + 1]);
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
 
@@ -111,13 +124,7 @@ __device__ __forceinline__ void store8_nt(E* p, const float* v) {
   } else {
     u32x4_t w;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const E lo = TypeOps<E>::from_f(v[2 * i]), hi = TypeOps<E>::from_f(v[2 * i + 1]);
-      uint16_t bl, bh;
-      __builtin_memcpy(&bl, &lo, 2);
-      __builtin_memcpy(&bh, &hi, 2);
-      w[i] = (uint32_t)bl | ((uint32_t)bh << 16);
-    }
+    for (int i = 0; i < 4; ++i) w[i] = pack2<E>(v[2 * i], v[2 * i + 1]);
     __builtin_nontemporal_store(w, (u32x4_t*)p);
   }
 }

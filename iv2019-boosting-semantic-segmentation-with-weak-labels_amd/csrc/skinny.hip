@@ -64,13 +64,7 @@ __global__ __launch_bounds__(SK_THREADS) void skinny_narrow_n_kernel(ConvArgs a)
     if (m < M && lq * 4 < N) {
       uint32_t w2[2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const E lo = TypeOps<E>::from_f(acc[2 * h]), hi = TypeOps<E>::from_f(acc[2 * h + 1]);
-        uint16_t bl, bh;
-        __builtin_memcpy(&bl, &lo, 2);
-        __builtin_memcpy(&bh, &hi, 2);
-        w2[h] = (uint32_t)bl | ((uint32_t)bh << 16);
-      }
+      for (int h = 0; h < 2; ++h) w2[h] = pack2<E>(acc[2 * h], acc[2 * h + 1]);
       *(uint2*)(Y + (size_t)m * a.ldy + lq * 4) = make_uint2(w2[0], w2[1]);
     }
 #pragma unroll

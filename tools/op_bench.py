@@ -42,6 +42,10 @@ def run():
     elif op == "dgrad":
         check(LIB.seg_op_conv_dgrad(1, dy.data_ptr(), N, H, W, Co, Co, wt.data_ptr(), Ci, k, s, r, 0,
                                     H, W, dx.data_ptr(), Ci, stream))
+    elif os.environ.get("SPLITS"):   # the 256 x 256 kernel at an explicit split count (side-stream sizing)
+        check(LIB.seg_op_conv_wgrad_cfg(1, dy.data_ptr(), N, H, W, Co, Co, x.data_ptr(), H, W, Ci, Ci,
+                                        k, s, r, 0, dw.data_ptr(), ws.data_ptr(), ws.numel(), 256, 256,
+                                        int(os.environ["SPLITS"]), stream))
     else:
         check(LIB.seg_op_conv_wgrad(1, dy.data_ptr(), N, H, W, Co, Co, x.data_ptr(), H, W, Ci, Ci,
                                     k, s, r, 0, dw.data_ptr(), ws.data_ptr(), ws.numel(), stream))
