@@ -34,8 +34,7 @@ struct BnApplyArgs {
 struct BnBwdArgs {
   const void* dz; int lddz;        // incoming gradient (T or f32)
   const void* z; int ldz;          // activation whose >0 mask gates dz (nullable)
-  const uint8_t* mask;             // the same gate as bits [M][ldm] (preferred over z when set)
-  int ldm;                         // bytes per mask row (0: C / 8); channel slabs keep the full row
+  const uint8_t* mask;             // the same gate as bits [M][C/8] (preferred over z when set)
   const void* y; int ldy;          // conv output (T)
   long M; int C;
   const float* mean; const float* invstd; const float* scale;

@@ -355,18 +355,6 @@ __global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
 // and walks rows; U rows are loaded before any is consumed, so U x (2..3) 16-B loads are in
 // flight per lane. No integer division in the row loop. C/8 > 256 spills into blockIdx.y.
 constexpr int BN_U = 4;   // rows in flight per thread (reduce combines 4 slots explicitly)
-// backward kernels (bwd_load, reduce8, apply8): rows in flight per thread and launch bounds.
-// A/B knob: SEG_BN_BWD_U=1 with SEG_BN_BWD_VGPRS=48 lets a backward workgroup sit
-// on a CU beside a weight-gradient ping-pong workgroup (2 x 232 VGPRs per SIMD)
-#ifndef SEG_BN_BWD_U
-#define SEG_BN_BWD_U 4
-#endif
-constexpr int BU = SEG_BN_BWD_U;
-#ifdef SEG_BN_BWD_VGPRS
-#define BN_BWD_LB __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(512 / SEG_BN_BWD_VGPRS, 512 / SEG_BN_BWD_VGPRS)))
-#else
-#define BN_BWD_LB __launch_bounds__(256)
-#endif
 
 struct RowLane {
   int cg, rl, rpp;
@@ -483,17 +471,17 @@ template <> struct Raw8<float> {
 // masked incoming gradient for n rows (dz * [z > 0] * dzscale) and the matching y rows
 template <typename T, typename TZ, int HZ, int HS, bool FULL>
 __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, int rpp, int nrows,
-                                         float (&dz)[BU][8], float (&y)[BU][8]) {
-  if constexpr (FULL) nrows = BU;
+                                         float (&dz)[BN_U][8], float (&y)[BN_U][8]) {
+  if constexpr (FULL) nrows = BN_U;
   const TZ* DZ = (const TZ*)a.dz + c0;
   const TZ* Z = (const TZ*)a.z + c0;
   const T* Y = (const T*)a.y + c0;
-  Raw8<TZ> rdz[BU], rz[BU];
-  Raw8<T> ry[BU];
-  uint32_t mk[BU];
-  const int cg = c0 >> 3, cgn = a.ldm ? a.ldm : a.C >> 3;
+  Raw8<TZ> rdz[BN_U], rz[BN_U];
+  Raw8<T> ry[BN_U];
+  uint32_t mk[BN_U];
+  const int cg = c0 >> 3, cgn = a.C >> 3;
 #pragma unroll
-  for (int k = 0; k < BU; ++k) {
+  for (int k = 0; k < BN_U; ++k) {
     if (FULL || k < nrows) {
       const size_t m = (size_t)(base + k * rpp);
       rdz[k].load(DZ + m * a.lddz);
@@ -504,7 +492,7 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
   }
   __builtin_amdgcn_sched_barrier(0);   // keep the group's loads ahead of every conversion
 #pragma unroll
-  for (int k = 0; k < BU; ++k) {
+  for (int k = 0; k < BN_U; ++k) {
     if (FULL || k < nrows) {
       rdz[k].cvt(dz[k]);
       ry[k].cvt(y[k]);
@@ -526,7 +514,7 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
     float ds[8];
     ld8(a.dzscale, c0, ds);
 #pragma unroll
-    for (int k = 0; k < BU; ++k)
+    for (int k = 0; k < BN_U; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) dz[k][e] *= ds[e];
   }
@@ -534,7 +522,7 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
 
 // per row block partial (sum dyhat, sum dyhat*xhat); rows of block b: [b*rows_per, ...)
 template <typename T, typename TZ, int HZ, int HS>
-__global__ BN_BWD_LB void bn_bwd_reduce8_kernel(BnBwdArgs a) {
+__global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
   __shared__ float sh[2][256 * 8];
   const RowLane L = row_lane(a.C / 8);
   const int c0 = (L.act ? L.cg : 0) * 8;
@@ -544,18 +532,18 @@ __global__ BN_BWD_LB void bn_bwd_reduce8_kernel(BnBwdArgs a) {
   float s1[8], s2[8], mu[8], inv[8];
   // one accumulator set per row slot k: the U rows of a group stay independent (no loop
   // rerolling), so their loads are issued together
-  float t1[BU][8], t2[BU][8];
+  float t1[BN_U][8], t2[BN_U][8];
 #pragma unroll
-  for (int k = 0; k < BU; ++k)
+  for (int k = 0; k < BN_U; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e) { t1[k][e] = 0.f; t2[k][e] = 0.f; }
   if (L.act) {
     ld8(a.mean, c0, mu); ld8(a.invstd, c0, inv);
     auto acc = [&](long base, int nrows, auto full) {
-      float dz[BU][8], y[BU][8];
+      float dz[BN_U][8], y[BN_U][8];
       bwd_load<T, TZ, HZ, HS, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
 #pragma unroll
-      for (int k = 0; k < BU; ++k)
+      for (int k = 0; k < BN_U; ++k)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           t1[k][e] += dz[k][e];
@@ -563,20 +551,13 @@ __global__ BN_BWD_LB void bn_bwd_reduce8_kernel(BnBwdArgs a) {
         }
     };
     long base = r0 + L.rl;
-    for (; base + (BU - 1) * L.rpp < r1; base += (long)L.rpp * BU) acc(base, BU, std::true_type{});
+    for (; base + (BN_U - 1) * L.rpp < r1; base += (long)L.rpp * BN_U) acc(base, BN_U, std::true_type{});
     if (base < r1) acc(base, (int)((r1 - base + L.rpp - 1) / L.rpp), std::false_type{});
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    if constexpr (BU == 4) {
-      s1[e] = (t1[0][e] + t1[1][e]) + (t1[2][e] + t1[3][e]);
-      s2[e] = (t2[0][e] + t2[1][e]) + (t2[2][e] + t2[3][e]);
-    } else {
-      s1[e] = t1[0][e];
-      s2[e] = t2[0][e];
-#pragma unroll
-      for (int k = 1; k < BU; ++k) { s1[e] += t1[k][e]; s2[e] += t2[k][e]; }
-    }
+    s1[e] = (t1[0][e] + t1[1][e]) + (t1[2][e] + t1[3][e]);
+    s2[e] = (t2[0][e] + t2[1][e]) + (t2[2][e] + t2[3][e]);
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -599,7 +580,7 @@ __global__ BN_BWD_LB void bn_bwd_reduce8_kernel(BnBwdArgs a) {
 }
 
 template <typename T, typename TZ, int HZ, int HS, int HD>
-__global__ BN_BWD_LB void bn_bwd_apply8_kernel(BnBwdArgs a) {
+__global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwdArgs a) {
   const RowLane L = row_lane(a.C / 8);
   if (!L.act) return;
   const int c0 = L.cg * 8;
@@ -610,13 +591,13 @@ __global__ BN_BWD_LB void bn_bwd_apply8_kernel(BnBwdArgs a) {
   T* DH = (T*)a.dyhat + c0;
   float ds[8];
   if constexpr (HS) ld8(a.dzscale, c0, ds);
-  const long step = (long)L.rpp * BU;
+  const long step = (long)L.rpp * BN_U;
   auto body = [&](long base, int nrows, auto full) {
-    float dz[BU][8], y[BU][8];
-    if constexpr (decltype(full)::value) nrows = BU;
+    float dz[BN_U][8], y[BN_U][8];
+    if constexpr (decltype(full)::value) nrows = BN_U;
     bwd_load<T, TZ, HZ, 0, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
 #pragma unroll
-    for (int k = 0; k < BU; ++k) {
+    for (int k = 0; k < BN_U; ++k) {
       if (k >= nrows) continue;
       const size_t m = (size_t)(base + k * L.rpp);
       // dyhat: the masked gradient before the per-channel factor (group norm's gamma)
@@ -635,7 +616,7 @@ __global__ BN_BWD_LB void bn_bwd_apply8_kernel(BnBwdArgs a) {
     }
   };
   long base = (long)blockIdx.x * step + L.rl;
-  for (; base + (BU - 1) * L.rpp < a.M; base += (long)gridDim.x * step) body(base, BU, std::true_type{});
+  for (; base + (BN_U - 1) * L.rpp < a.M; base += (long)gridDim.x * step) body(base, BN_U, std::true_type{});
   if (base < a.M) body(base, (int)((a.M - base + L.rpp - 1) / L.rpp), std::false_type{});
 }
 
@@ -660,7 +641,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_dual_kernel(BnBwdArgs a) {
     const T* DZ = (const T*)a.dz + c0;
     const T* Y = (const T*)a.y + c0;
     const T* Y2 = (const T*)a.y2 + c0;
-    const int cg = c0 >> 3, cgn = a.ldm ? a.ldm : a.C >> 3;
+    const int cg = c0 >> 3, cgn = a.C >> 3;
     for (long base = r0 + L.rl; base < r1; base += (long)L.rpp * U) {
       Raw8<T> rdz[U], ry[U], ry2[U];
       uint32_t mk[U];
@@ -735,7 +716,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_dual_kernel(BnBwdArgs a) {
   const T* Y2 = (const T*)a.y2 + c0;
   T* DY = (T*)a.dy + c0;
   T* DY2 = (T*)a.dy2 + c0;
-  const int cg = c0 >> 3, cgn = a.ldm ? a.ldm : a.C >> 3;
+  const int cg = c0 >> 3, cgn = a.C >> 3;
   const long step = (long)L.rpp * U;
   for (long base = (long)blockIdx.x * step + L.rl; base < a.M; base += (long)gridDim.x * step) {
     Raw8<T> rdz[U], ry[U], ry2[U];

@@ -462,10 +462,6 @@ WgradArgs wgrad_problem(const ConvL& L, bool s2d) {
   return a;
 }
 
-#ifndef SEG_BN_SLAB_MB
-#define SEG_BN_SLAB_MB 0   // BN-backward channel slabs (bn_backward); 0 = whole layers
-#endif
-
 // ------------------------------------------------------------------------------------------
 // kernel sequencing helpers
 // ------------------------------------------------------------------------------------------
@@ -623,58 +619,29 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   a.part = L.bwd_part; a.rb = L.rb;
   a.dzscale = dzscale;
   const double esz = seg_half(S.dt) ? 2.0 : 4.0, zsz = dz_f32 ? 4.0 : esz;
+  const double me = a.M * (double)a.C * 1e-9;
+  const double gb_in = me * (zsz + (a.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
+  int slot;
+  if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
+  HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
   const bool tb = c->cfg.train_bn != 0;
-  // channel slabs (SEG_BN_SLAB_MB): reduce -> finalize -> apply per slab of channels whose
-  // dz + y bytes fit the Infinity Cache, so the apply's re-read of them is served on-die
-  int cs = a.C;
-  const double row_b = (zsz + esz) * (double)a.M;
-  if (SEG_BN_SLAB_MB > 0 && !c->sync_fn && !dz_f32 && a.C % 64 == 0 &&
-      row_b * a.C > SEG_BN_SLAB_MB * 1048576.0) {
-    cs = (int)(SEG_BN_SLAB_MB * 1048576.0 / row_b) / 64 * 64;
-    if (cs < 64) cs = 64;
-    while (a.C % cs) cs -= 64;   // equal slabs
+  // a backward after a moving-statistics forward (TRAIN without
+  // batch_norm_accumulate_statistics) differentiates through constant statistics
+  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
+                                    tb ? c->grads + L.g_off : nullptr,
+                                    tb ? c->grads + L.b_off : nullptr, S.s, c->bn_infer));
+  if (c->sync_fn && !c->bn_infer) {
+    // [mean(dyhat) | mean(dyhat * xhat)] (contiguous in the layer's state) averaged over the
+    // replicas: dx is the gradient through the global statistics; dgamma / dbeta stay this
+    // replica's sums (the gradient all-reduce averages them)
+    if (int r = sync_exchange(c, L.st.sdy, 2L * L.co, S.s)) return r;
+    HIPCALL(c, launch_scale2(L.st.sdy, 2L * L.co, 1.f / c->sync_world, 0, 1.f, S.s));
   }
-  if (a.mask && cs < a.C) a.ldm = a.C / 8;
-  for (int c0 = 0; c0 < a.C; c0 += cs) {
-    BnBwdArgs b = a;
-    BnState st = L.st;
-    if (cs < a.C) {
-      const size_t eo = (size_t)c0 * (size_t)(dz_f32 ? 4 : c->esz), ey = (size_t)c0 * c->esz;
-      b.dz = (const char*)a.dz + eo;
-      if (a.z) b.z = (const char*)a.z + eo;
-      if (a.mask) b.mask = a.mask + c0 / 8;
-      b.y = (const char*)a.y + ey;
-      b.dy = (char*)a.dy + ey;
-      if (a.dyhat) b.dyhat = (char*)a.dyhat + ey;
-      if (a.dzscale) b.dzscale = a.dzscale + c0;
-      b.C = cs;
-      st.mean += c0; st.invstd += c0; st.scale += c0; st.var_unb += c0; st.sdy += c0; st.sdyx += c0;
-      b.mean = st.mean; b.invstd = st.invstd; b.scale = st.scale; b.sdy = st.sdy; b.sdyx = st.sdyx;
-    }
-    const double me = b.M * (double)b.C * 1e-9;
-    const double gb_in = me * (zsz + (b.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
-    int slot;
-    if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
-    HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, b, S.s));
-    if (int r = prof_end(c, S.s, slot)) return r;
-    // a backward after a moving-statistics forward (TRAIN without
-    // batch_norm_accumulate_statistics) differentiates through constant statistics
-    HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, b.M, b.C, st,
-                                      tb ? c->grads + L.g_off + c0 : nullptr,
-                                      tb ? c->grads + L.b_off + c0 : nullptr, S.s, c->bn_infer));
-    if (c->sync_fn && !c->bn_infer) {
-      // [mean(dyhat) | mean(dyhat * xhat)] (contiguous in the layer's state) averaged over the
-      // replicas: dx is the gradient through the global statistics; dgamma / dbeta stay this
-      // replica's sums (the gradient all-reduce averages them)
-      if (int r = sync_exchange(c, L.st.sdy, 2L * L.co, S.s)) return r;
-      HIPCALL(c, launch_scale2(L.st.sdy, 2L * L.co, 1.f / c->sync_world, 0, 1.f, S.s));
-    }
-    const double gb_apply = gb_in + me * esz * (dyhat_out ? 2 : 1);
-    if (int r = prof_begin(c, S.s, 5, li, gb_apply, &slot)) return r;
-    HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, b, S.s));
-    if (int r = prof_end(c, S.s, slot)) return r;
-  }
-  return 0;
+  const double gb_apply = gb_in + me * esz * (dyhat_out ? 2 : 1);
+  if (int r = prof_begin(c, S.s, 5, li, gb_apply, &slot)) return r;
+  HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
+  return prof_end(c, S.s, slot);
 }
 
 // BN backward of two layers gated by the same dz / ReLU bits (a projection unit's conv3 and
@@ -698,48 +665,21 @@ int bn_backward_dual(Step& S, int li, int li2, const Act& dz, const Act& z) {
   a.dy2 = L2.dy.p; a.lddy2 = L2.dy.ld;
   a.part2 = L2.bwd_part;
   const double esz = seg_half(S.dt) ? 2.0 : 4.0;
+  const double me = a.M * (double)a.C * 1e-9;
+  const double gb_in = me * (esz + 0.125 + 2 * esz);   // dz + bits + both y
+  int slot;
+  if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
+  HIPCALL(c, launch_bn_bwd_reduce_dual(S.dt, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
   const bool tb = c->cfg.train_bn != 0;
-  // channel slabs as in bn_backward (dz + both y per slab within SEG_BN_SLAB_MB)
-  int cs = a.C;
-  const double row_b = 3.0 * esz * (double)a.M;
-  if (SEG_BN_SLAB_MB > 0 && a.C % 64 == 0 && row_b * a.C > SEG_BN_SLAB_MB * 1048576.0) {
-    cs = (int)(SEG_BN_SLAB_MB * 1048576.0 / row_b) / 64 * 64;
-    if (cs < 64) cs = 64;
-    while (a.C % cs) cs -= 64;
-  }
-  if (cs < a.C) a.ldm = a.C / 8;
-  for (int c0 = 0; c0 < a.C; c0 += cs) {
-    BnBwdArgs b = a;
-    BnState st = L.st, st2 = L2.st;
-    if (cs < a.C) {
-      const size_t eo = (size_t)c0 * c->esz;
-      b.dz = (const char*)a.dz + eo; b.mask = a.mask + c0 / 8;
-      b.y = (const char*)a.y + eo; b.y2 = (const char*)a.y2 + eo;
-      b.dy = (char*)a.dy + eo; b.dy2 = (char*)a.dy2 + eo;
-      b.C = cs;
-      for (BnState* q : {&st, &st2}) {
-        q->mean += c0; q->invstd += c0; q->scale += c0; q->var_unb += c0; q->sdy += c0; q->sdyx += c0;
-      }
-      b.mean = st.mean; b.invstd = st.invstd; b.scale = st.scale; b.sdy = st.sdy; b.sdyx = st.sdyx;
-      b.mean2 = st2.mean; b.invstd2 = st2.invstd; b.scale2 = st2.scale; b.sdy2 = st2.sdy;
-      b.sdyx2 = st2.sdyx;
-    }
-    const double me = b.M * (double)b.C * 1e-9;
-    const double gb_in = me * (esz + 0.125 + 2 * esz);   // dz + bits + both y
-    int slot;
-    if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
-    HIPCALL(c, launch_bn_bwd_reduce_dual(S.dt, b, S.s));
-    if (int r = prof_end(c, S.s, slot)) return r;
-    HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, b.M, b.C, st, tb ? c->grads + L.g_off + c0 : nullptr,
-                                      tb ? c->grads + L.b_off + c0 : nullptr, S.s, c->bn_infer));
-    HIPCALL(c, launch_bn_bwd_finalize(L2.bwd_part, L2.rb, b.M, b.C, st2,
-                                      tb ? c->grads + L2.g_off + c0 : nullptr,
-                                      tb ? c->grads + L2.b_off + c0 : nullptr, S.s, c->bn_infer));
-    if (int r = prof_begin(c, S.s, 5, li, gb_in + me * 2 * esz, &slot)) return r;
-    HIPCALL(c, launch_bn_bwd_apply_dual(S.dt, b, S.s));
-    if (int r = prof_end(c, S.s, slot)) return r;
-  }
-  return 0;
+  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st, tb ? c->grads + L.g_off : nullptr,
+                                    tb ? c->grads + L.b_off : nullptr, S.s, c->bn_infer));
+  HIPCALL(c, launch_bn_bwd_finalize(L2.bwd_part, L2.rb, a.M, L2.co, L2.st,
+                                    tb ? c->grads + L2.g_off : nullptr,
+                                    tb ? c->grads + L2.b_off : nullptr, S.s, c->bn_infer));
+  if (int r = prof_begin(c, S.s, 5, li, gb_in + me * 2 * esz, &slot)) return r;
+  HIPCALL(c, launch_bn_bwd_apply_dual(S.dt, a, S.s));
+  return prof_end(c, S.s, slot);
 }
 
 // group norm backward (gn.h): per image the batch-norm reduce (S1, S2 per channel) into
