@@ -11,5 +11,5 @@ for spec in "wgrad b4c2" "fwd b4c3" "dgrad b4c1" "wgrad b3c1"; do
   set -- $spec
   echo "pmc $1 $2" && tools/pmc_passes.sh $out/pmc_$1_$2 $1 $2 && python3 tools/rocpd_pmc.py $out/pmc_$1_$2 conv > $out/pmc_$1_$2.txt && rm -rf $out/pmc_$1_$2
 done
-echo timeline; bash tools/timeline_pass.sh ${1:-final_prof}_tl
+echo timeline; bash tools/timeline_pass.sh $(basename $out)_tl
 echo done
