@@ -82,22 +82,25 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// v[r] += v[r] of the DPP partner lane, as one v_add_f32_dpp per value (the builtin form
-// was a v_mov_b32_dpp + v_add pair). The s_nop covers the VALU-write -> DPP-read hazard of the
-// previous step's results (inline asm is opaque to the hazard recognizer).
-#define PP_ROW_SUM(CTRL)                                                                 \
-  asm volatile("s_nop 1\n"                                                              \
-               "v_add_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n"          \
-               "v_add_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf\n"          \
-               "v_add_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf\n"          \
-               "v_add_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf"             \
-               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]))
-__device__ __forceinline__ void row_total(float (&v)[4]) {
-  PP_ROW_SUM("quad_perm:[1,0,3,2]");
-  PP_ROW_SUM("quad_perm:[2,3,0,1]");
-  PP_ROW_SUM("row_half_mirror");
-  PP_ROW_SUM("row_mirror");
-  asm volatile("s_nop 1" ::: "memory");   // the results feed ordinary VALU reads / DPP next
+// v[r] += v[r] of the DPP partner lane, as one v_add_f32_dpp per value (the builtin form was a
+// v_mov_b32_dpp + v_add pair), 4 butterfly steps over 8 values in one block: a value's next
+// step is 8 instructions after its previous one, so only the block's entry and exit need the
+// s_nop for the VALU-write -> DPP-read hazard (inline asm is opaque to the hazard recognizer;
+// the 4-value form needed one per step)
+#define PP_ROW_SUM8(CTRL)                                                           \
+  "v_add_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n"                   \
+  "v_add_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf\n"                   \
+  "v_add_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf\n"                   \
+  "v_add_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf\n"                   \
+  "v_add_f32_dpp %4, %4, %4 " CTRL " row_mask:0xf bank_mask:0xf\n"                   \
+  "v_add_f32_dpp %5, %5, %5 " CTRL " row_mask:0xf bank_mask:0xf\n"                   \
+  "v_add_f32_dpp %6, %6, %6 " CTRL " row_mask:0xf bank_mask:0xf\n"                   \
+  "v_add_f32_dpp %7, %7, %7 " CTRL " row_mask:0xf bank_mask:0xf\n"
+__device__ __forceinline__ void row_total8(float (&v)[8]) {
+  asm volatile("s_nop 1\n" PP_ROW_SUM8("quad_perm:[1,0,3,2]") PP_ROW_SUM8("quad_perm:[2,3,0,1]")
+               PP_ROW_SUM8("row_half_mirror") PP_ROW_SUM8("row_mirror") "s_nop 1"
+               : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                 "+v"(v[7]));
 }
 
 // PERSIST: loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
@@ -430,34 +433,54 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     // half between that half's staging writes and the barrier, so the VALU work overlaps the
     // LDS traffic and the other waves' arrival
     const bool full = nvalid == 128;
+    auto store_stats = [&](const int qn, const int j, const float* sm, const float* m2) {
+      const int n = nbase + qn * 128 + j * 16;
+      if (lr == 0 && n < a.Co) {
+        float* dst = a.stats + 2 * ((size_t)(mt * 2 + wm) * a.Co + n);
+        *(float4*)dst = make_float4(sm[0], m2[0], sm[1], m2[1]);
+        *(float4*)(dst + 4) = make_float4(sm[2], m2[2], sm[3], m2[3]);
+      }
+    };
     auto stats_half = [&](const int qn) {
+      if (full) {
+        // exact two-pass moments over the wave row's 128 rows, both column fragments j at once:
+        // the 8 rows of the lane are summed, the sums are completed over the 16 lanes of the
+        // row group by a DPP-add butterfly (quad_perm xor 1, xor 2, row_half_mirror,
+        // row_mirror: every lane ends with the totals), then the squared deviations from those
+        // means the same way
+        float sm[8], m2[8];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4_t s4 = acc[0][qn][0][j];
+#pragma unroll
+          for (int f = 1; f < 8; ++f) s4 += acc[f >> 2][qn][f & 3][j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sm[j * 4 + r] = s4[r];
+        }
+        row_total8(sm);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4_t mu;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mu[r] = sm[j * 4 + r] * (1.f / 128.f);
+          f32x4_t q4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int f = 0; f < 8; ++f) {
+            const f32x4_t d = acc[f >> 2][qn][f & 3][j] - mu;
+            q4 += d * d;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) m2[j * 4 + r] = q4[r];
+        }
+        row_total8(m2);
+        store_stats(qn, 0, sm, m2);
+        store_stats(qn, 1, sm + 4, m2 + 4);
+        return;
+      }
   #pragma unroll
         for (int j = 0; j < 2; ++j) {
           float sm[4], m2[4];
-          if (full) {
-            // exact two-pass moments over the wave row's 128 rows: the 8 rows of the lane are
-            // summed, the sum is completed over the 16 lanes of the row group by a DPP-add
-            // butterfly (quad_perm xor 1, xor 2, row_half_mirror, row_mirror: every lane ends
-            // with the total), then the squared deviations from that mean the same way
-            f32x4_t s4 = acc[0][qn][0][j];
-#pragma unroll
-            for (int f = 1; f < 8; ++f) s4 += acc[f >> 2][qn][f & 3][j];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sm[r] = s4[r];
-            row_total(sm);
-            f32x4_t mu;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mu[r] = sm[r] * (1.f / 128.f);
-            f32x4_t q4 = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int f = 0; f < 8; ++f) {
-              const f32x4_t d = acc[f >> 2][qn][f & 3][j] - mu;
-              q4 += d * d;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) m2[r] = q4[r];
-            row_total(m2);
-          } else {
+          {
             // ragged last tile: per-lane counts, general merges
             int c = 0;
   #pragma unroll
@@ -500,12 +523,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
               nn = nn + n2;
             }
           }
-          const int n = nbase + qn * 128 + j * 16;
-          if (lr == 0 && n < a.Co) {
-            float* dst = a.stats + 2 * ((size_t)(mt * 2 + wm) * a.Co + n);
-            *(float4*)dst = make_float4(sm[0], m2[0], sm[1], m2[1]);
-            *(float4*)(dst + 4) = make_float4(sm[2], m2[2], sm[3], m2[3]);
-          }
+          store_stats(qn, j, sm, m2);
         }
     };
     PP_TS(dbg_it, 2);
@@ -1015,6 +1033,29 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
 
   float* O = a.out + (size_t)split * a.Co * Ncol;
   const int lr = lane & 15;
+  if (m0 + BM <= a.Co && n0 + BN <= Ncol && (long)a.Co * Ncol * 4 < (1L << 31)) {
+    // whole tile: buffer stores with the row offset in an SGPR (one per (qm, i, r), shared by
+    // the qn / j stores) and the column in the immediate; the checked form below spent ~9
+    // instructions per value (bounds compare, exec mask, 64-bit multiply-add) on 128 values
+    // per lane, 10 % of a 32-K-tile 1x1 launch
+    const auto rs_o = __builtin_amdgcn_make_buffer_rsrc((void*)O, (short)0, (int)((long)a.Co * Ncol * 4), 0x00020000);
+    const uint32_t vb = (uint32_t)(((m0 + wm * 64 + lq * 4) * Ncol + n0 + wn * 32 + lr) * 4);
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int so = __builtin_amdgcn_readfirstlane((qm * 128 + i * 16 + r) * Ncol * 4);
+#pragma unroll
+          for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[qm][qn][i][j][r]), rs_o,
+                                                    vb + (qn * 128 + j * 16) * 4, so, 0);
+        }
+    return;
+  }
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm)
 #pragma unroll

@@ -1111,6 +1111,22 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
 
   float* O = a.out + (size_t)split * a.Co * Ncol;
   const int lr = lane & 15;
+  if (m0 + BM <= a.Co && n0 + BN <= Ncol && (long)a.Co * Ncol * 4 < (1L << 31)) {
+    // whole tile: buffer stores, row offset in an SGPR, column in the immediate (as
+    // conv_wgrad_pp_body)
+    const auto rs_o = __builtin_amdgcn_make_buffer_rsrc((void*)O, (short)0, (int)((long)a.Co * Ncol * 4), 0x00020000);
+    const uint32_t vb = (uint32_t)(((m0 + wm * WM + lq * 4) * Ncol + n0 + wn * WN + lr) * 4);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int so = __builtin_amdgcn_readfirstlane((i * 16 + r) * Ncol * 4);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), rs_o, vb + j * 16 * 4, so, 0);
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll

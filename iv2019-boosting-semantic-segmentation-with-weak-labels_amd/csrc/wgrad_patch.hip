@@ -197,14 +197,18 @@ __global__ __launch_bounds__(WP_THREADS, 1) void conv_wgrad_patch_kernel(WgradAr
   const int Ncol = 9 * a.C;
   float* O = a.out + (size_t)split * a.Co * Ncol;
   const int lr = lane & 15;
+  // buffer stores: per-lane base (co row group, ci), (f, tap, r) as an SGPR offset (the 64-bit
+  // index math per value was ~5 instructions of 72 stores per lane)
+  const auto rs_o = __builtin_amdgcn_make_buffer_rsrc((void*)O, (short)0, (int)((long)a.Co * Ncol * 4), 0x00020000);
+  const uint32_t vb = (uint32_t)(((co0 + wco * 32 + lq * 4) * Ncol + ci0 + wci * 16 + lr) * 4);
 #pragma unroll
   for (int f = 0; f < 2; ++f)
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco * 32 + f * 16 + lq * 4 + r;
-        O[(size_t)co * Ncol + tp * a.C + ci0 + wci * 16 + lr] = acc[f][tp][r];
+        const int so = __builtin_amdgcn_readfirstlane(((f * 16 + r) * Ncol + tp * a.C) * 4);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[f][tp][r]), rs_o, vb, so, 0);
       }
 }
 
