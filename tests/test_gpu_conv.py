@@ -22,6 +22,7 @@ CASES = [
     (2, 9, 10, 256, 3, 1, 1, 1, False),       # l2 human logits
     (1, 6, 6, 1280, 256, 1, 1, 1, False),     # PSP final (C=1280)
     (2, 15, 21, 256, 512, 1, 1, 1, False),    # short K, wide N: 128-row tiles, 2 per CU
+    (1, 20, 20, 128, 256, 1, 1, 1, False),    # ping-pong tile whose second wave row is ragged (16 rows)
     # small-channel 3x3 patch kernel (8 x 32 pixel tiles, input patch staged once per chunk)
     (2, 16, 64, 64, 64, 3, 1, 1, False),      # one 64-channel chunk, Co 64
     (1, 24, 96, 128, 128, 3, 1, 1, False),    # two chunks (second patch streamed), Co 128
