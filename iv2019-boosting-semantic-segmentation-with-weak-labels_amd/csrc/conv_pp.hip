@@ -37,6 +37,20 @@ __device__ unsigned long long g_pp_dbg[256 * 16 * 4];
 #define PP_TS(it, k)
 #endif
 
+#ifdef NT_DBG_TIMING
+// A/B only: per-wave segment timestamps (s_memtime) of the NT ping-pong loop, blocks 0-7, the
+// first tile, 8 K-tiles from K-tile 16 (or 0 when the tile has fewer than 24), 8 stamps per
+// K-tile (loop top, before / after barrier A, after the first MFMA segment, after barrier B,
+// before / after barrier C, after the second MFMA segment)
+__device__ unsigned long long g_nt_dbg[8 * 8 * 8 * 8];
+#define NT_TS(kb, k)                                                                             \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 8 && dbg_it == 0 && (kb) >= nt_kb0 && (kb) < nt_kb0 + 8) \
+    g_nt_dbg[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + ((kb) - nt_kb0)) * 8 + (k)] =            \
+        __builtin_amdgcn_s_memtime()
+#else
+#define NT_TS(kb, k)
+#endif
+
 #ifdef WG_DBG_TIMING
 // A/B only: per-wave segment timestamps (s_memtime) of the wgrad ping-pong loop, blocks 0-7,
 // K-tiles 16-23, 8 stamps per K-tile (loop top, before / after barrier A, after the first MFMA
@@ -359,9 +373,13 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     // LDS reads complete, so a DMA issued after the next barrier cannot overwrite a half that
     // another wave is still reading
     KT tn1{};
+#ifdef NT_DBG_TIMING
+    const int nt_kb0 = nk >= 24 ? 16 : 0;
+#endif
     for (int kb = 0; kb < nk; ++kb) {
       const char* buf = smem + (kb & 1) * BUF;
       const bool m1 = kb + 1 < nk, m2 = kb + 2 < nk;
+      NT_TS(kb, 0);
       read_a(buf, 0);
       read_b(buf, 0);
       read_b(buf, 1);
@@ -379,14 +397,18 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      NT_TS(kb, 1);
       pp_barrier();
+      NT_TS(kb, 2);
       mfma_q(0, 0);
       mfma_q(0, 1);
       if (wm == 0) {
         if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      NT_TS(kb, 3);
       pp_barrier();
+      NT_TS(kb, 4);
       read_a(buf, 1);
       if (m2) {
         tn1 = ktile_next();
@@ -398,9 +420,12 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         if (m2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       }
+      NT_TS(kb, 5);
       pp_barrier();
+      NT_TS(kb, 6);
       mfma_q(1, 1);
       mfma_q(1, 0);
+      NT_TS(kb, 7);
       if (m1 && wm == 0) {
         if (m2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -1108,6 +1133,12 @@ hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s) {
   if (a.Wo >= 64) return launch(conv_wgrad_pp_kernel<bf16_t, 1>);
   return launch(conv_wgrad_pp_kernel<bf16_t, 0>);
 }
+
+#ifdef NT_DBG_TIMING
+extern "C" int seg_dbg_nt_timing(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nt_dbg), sizeof(g_nt_dbg)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef WG_DBG_TIMING
 extern "C" int seg_dbg_wg_timing(void* host) {
