@@ -234,10 +234,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU (the driver's launch); more ranks than GPUs only for the one-GPU
+    # rehearsal of the N > 1 path (SEG_BENCH_BACKEND=gloo: RCCL does not share a device)
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if ndev else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
+    backend = os.environ.get("SEG_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from estimator.define_estimator_hierarchical import allreduce_grads
     from input_pipelines.synthetic import batch
@@ -257,7 +265,7 @@ def main():
     # num_updates = global_step, in UPDATE_OPS); MirroredStrategy runs drop it
     ema_on = world == 1
     ctx = SegContext(depth=depth, pyramid=args.pyramid, height=H, width=W, nb_pp=nb_pp, nb_pb=nb_pb,
-                     nb_pi=nb_pi, dtype=args.dtype, device=local, ema=ema_on)
+                     nb_pi=nb_pi, dtype=args.dtype, device=local_dev, ema=ema_on)
     ctx.load_params(init_params(ctx.param_info, seed=0))
     if world == 1 and args.dtype != "fp16" and not args.no_defer_stem:
         # single process: the update of every parameter but the stem's runs beside the stem's
