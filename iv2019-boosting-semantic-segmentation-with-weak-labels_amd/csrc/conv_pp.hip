@@ -64,12 +64,6 @@ __device__ unsigned long long g_wg_dbg[8 * 8 * 8 * 8];
 #define WG_TS(kb, k)
 #endif
 
-// NT main-loop wave priority: 1 = the lagging wave row (waves 4-7) at s_setprio 1 for the whole
-// main loop (the weight-gradient kernel's form); 0 = every MFMA segment raised and lowered (A/B)
-#ifndef SEG_NT_STATIC_PRIO
-#define SEG_NT_STATIC_PRIO 1
-#endif
-
 namespace {
 
 constexpr int PP_THREADS = 512;
@@ -311,7 +305,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     }
   };
   auto mfma_q = [&](int qm, int qn) {
-    if (!SEG_NT_STATIC_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -321,7 +314,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
           // transposed accumulators (lane = 4 channels of one pixel) for the register-side
           // statistics and 8-byte staging writes
           acc[qm][qn][i][j] = Half<E>::mma(bfq[qn][j][s], af[i][s], acc[qm][qn][i][j]);
-    if (!SEG_NT_STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   // ---- prologue of a tile: K-tile 0, halves in issue order A0, B0, B1, A1 ----
@@ -371,7 +363,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   if (wm == 1) pp_barrier();   // stagger: wave row 1 runs one segment behind
   // the lagging row loses every issue arbitration at equal priority: one static raise for the
   // main loop instead of per-segment flips (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (SEG_NT_STATIC_PRIO && wm == 1) __builtin_amdgcn_s_setprio(1);
+  if (wm == 1) __builtin_amdgcn_s_setprio(1);
 
   {
     // two phases per K-tile (half the barriers): phase 0 = quadrants (0,0), (0,1) from A0, B0,
@@ -443,7 +435,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     }
   }
   if (wm == 0) pp_barrier();   // realign the two wave rows: every LDS read of the tile is done
-  if (SEG_NT_STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_s_setprio(0);
   PP_TS(dbg_it, 1);
   // next tile: its K-tile 0 goes into buffer 0 now, in flight during this tile's epilogue
   const int tile_n = tile + (int)gridDim.x;
