@@ -601,3 +601,60 @@ def test_frozen_bn_train_step_fp32(cuda):
     for k in params:
         if "moving" in k:
             assert np.array_equal(nat["params"][k], params[k].reshape(-1)), k
+
+
+# the loss head's gradient w.r.t. the low-resolution logits (grad_un x dzscale: the gradient seed
+# of the backward), against autograd of the oracle's losses on the SAME native logits and under
+# the native l1 gate (define_losses_hierarchical.py:98-210 + the align-corners upsampler,
+# hierarchical.py:143-184). Nothing upstream of the logits enters, so this is well conditioned
+# (unlike the parameter gradients above) and held at 1e-5 per head (measured 0.6-1.7e-7 on one
+# box, profiles/r04_loss_grad.txt).
+LOSS_GRAD = [SegConfig(height=48, width=64, nb_pp=1, nb_pb=1, pyramid="none"),
+             SegConfig(height=64, width=96, nb_pp=1, nb_pb=1, nb_pi=1, pyramid="psp"),
+             SegConfig(height=64, width=128, nb_pp=2, pyramid="aspp")]
+
+
+@pytest.mark.parametrize("cfg", LOSS_GRAD, ids=lambda c: f"{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}")
+def test_loss_head_gradient_fp32(cuda, cfg):
+    from input_pipelines.synthetic import batch
+    from seg_hip import SegContext
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=3).items()}
+    data = batch(11, cfg.nb_pp, cfg.nb_pb, cfg.nb_pi, cfg.height, cfg.width)
+    ctx = SegContext(depth=cfg.depth, pyramid=cfg.pyramid, height=cfg.height, width=cfg.width,
+                     nb_pp=cfg.nb_pp, nb_pb=cfg.nb_pb, nb_pi=cfg.nb_pi, dtype="fp32",
+                     weight_decay=cfg.weight_decay, bn_decay=cfg.bn_decay)
+    ctx.load_params(params)
+    img = torch.as_tensor(data["images"]).to(cuda)
+    px = torch.as_tensor(data["px"]).to(cuda)
+    bb = torch.as_tensor(data["bbox"]).to(cuda) if cfg.nb_pb else None
+    tg = torch.as_tensor(data["tag"]).to(cuda) if cfg.nb_pi else None
+    ctx.forward(img)
+    ctx.loss(px, bb, tg)
+    hd = torch.empty((cfg.nb, cfg.height, cfg.width, 3), dtype=torch.int32, device=cuda)
+    ctx.full_predictions(head_decisions=hd)
+    losses, _, logits = ctx.outputs()
+    torch.cuda.synchronize()
+    lv = losses.cpu().numpy().copy()
+    c1, c2, c3 = 14, 7, 3
+    lg = logits[..., :c1 + c2 + c3].double().cpu()
+    g_nat = ctx.debug_tensor("grad_un")[..., :c1 + c2 + c3].astype(np.float64) * \
+        ctx.debug_tensor("dzscale").reshape(-1)[:c1 + c2 + c3].astype(np.float64)
+    d1 = hd[cfg.nb_pp:, ..., 0].cpu().numpy().astype(np.int64)
+    ctx.close()
+    net = OracleNet(cfg, params)
+    low, c0 = {}, 0
+    for key, c in (("l1_logits", c1), ("l2_vehicle_logits", c2), ("l2_human_logits", c3)):
+        low[key] = lg[..., c0:c0 + c].permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+        c0 += c
+    L = net.losses(low, data["px"], data.get("bbox"), data.get("tag"),
+                   weak_l1_decisions=d1 if cfg.nb_pb + cfg.nb_pi else None)
+    # the captured decisions are the loss head's own: counts under them equal the native ones
+    assert tuple(int(v) for v in L["counts"]) == tuple(int(v) for v in lv[4:7])
+    L["segmentation"].backward()
+    c0 = 0
+    for key, c in (("l1_logits", c1), ("l2_vehicle_logits", c2), ("l2_human_logits", c3)):
+        ref = low[key].grad.permute(0, 2, 3, 1).numpy()
+        err = _rel(g_nat[..., c0:c0 + c], ref)
+        print(f"{key}: rel {err:.2e} |g| {np.linalg.norm(ref):.3e}")
+        assert err < 1e-5, (key, err)
+        c0 += c
