@@ -513,7 +513,8 @@ __global__ __launch_bounds__(NT_THREADS, 2) void conv_wgrad_kernel(WgradArgs a) 
 
 __global__ void splitk_reduce_kernel(const float* __restrict__ part, int splits, long stride,
                                      long n, float* __restrict__ out, int accumulate) {
-  long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t * 4 < n; t += (long)gridDim.x * blockDim.x) {
+  const long i4 = t * 4;
   if (i4 + 3 < n && (stride & 3) == 0) {
     float4 s = accumulate ? *(const float4*)(out + i4) : make_float4(0.f, 0.f, 0.f, 0.f);
     // loads of 8 slabs in flight, summed in slab order (same result as the serial loop)
@@ -536,6 +537,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ part, int splits,
       for (int z = 0; z < splits; ++z) s += part[(size_t)z * stride + i];
       out[i] = s;
     }
+  }
   }
 }
 
@@ -801,7 +803,13 @@ hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s) {
 hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride, long n,
                                 float* out, int accumulate, hipStream_t s) {
   long threads = (n + 3) / 4;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ceil_div(threads, 256)), dim3(256), 0, s, part,
+  // at most 512 grid-stride workgroups: the reduces run on the weight-gradient stream beside the
+  // data-gradient chain, and a full-size grid (one float4 per thread, up to ~2300 workgroups)
+  // takes CUs from it in one burst; 256 / 512 / 1024 measured +0.2-0.3 % per step against the
+  // full grid, 128 -0.1 % (profiles/r04_splitk_grid.txt); per-element sums unchanged
+  long blocks = ceil_div(threads, 256);
+  if (blocks > 512) blocks = 512;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, part,
                      splits, split_stride, n, out, accumulate);
   return hipGetLastError();
 }
