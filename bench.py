@@ -1,8 +1,13 @@
 """Training-throughput benchmark of the MI355X path (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N
-          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+
+N > 1: `python bench.py --gpus N` launches N fresh rank processes itself (one per GPU, RCCL),
+as the reference's --distribute takes every visible GPU in one launch (system_factory.py:
+279-281); the parent never touches the GPU, re-prints rank 0's JSON line and fails if any rank
+fails. Under an external launcher (python -m torch.distributed.run --nnodes=1 --nproc-per-node
+N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...) WORLD_SIZE is set and must
+equal --gpus.
 
 Workload (BASELINE config C2, the metric's single-GPU configuration): ResNet-50 dilated
 (output stride 8) + ASPP (as C2 names it; the reference's commented-out _create_aspp_module,
@@ -207,6 +212,75 @@ def train_py_leg(args, steps=10, warmup=3):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without WORLD_SIZE: start N child processes of this script (never an
+    exec of this one), rank r on GPU r, rendezvous on 127.0.0.1. Runs before anything in this
+    process touches the GPU. Returns the exit code: 0 only if every rank exited 0 and rank 0
+    printed the JSON line (re-printed here on stdout). A failing rank stops the others."""
+    import signal
+    import socket
+    import subprocess
+    import tempfile
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    tmp = tempfile.mkdtemp(prefix="seg_bench_ranks_")
+    procs, outs = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = open(os.path.join(tmp, f"rank{r}.out"), "w+")
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=out, start_new_session=True))
+    rc = 0
+    try:
+        live = set(range(n))
+        while live:
+            for r in sorted(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.discard(r)
+                if c != 0:
+                    print(f"bench.py: rank {r} exited with {c}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    rc = rc or (c if c > 0 else 1)
+            if rc:
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except OSError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    line = None
+    for r, out in enumerate(outs):
+        out.seek(0)
+        for ln in out.read().splitlines():
+            if r == 0 and ln.startswith('{"metric"'):
+                line = ln
+            else:
+                print(f"[rank {r}] {ln}", file=sys.stderr)
+        out.close()
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    if rc == 0 and line is None:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr)
+        rc = 1
+    if line is not None and rc == 0:
+        print(line, flush=True)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -226,21 +300,32 @@ def main():
     ap.add_argument("--no-defer-stem", action="store_true",
                     help="A/B: join every weight gradient before the update (the N > 1 order)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
 
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("SEG_BENCH_BACKEND", "nccl")
     # one rank per GPU (the driver's launch); more ranks than GPUs only for the one-GPU
     # rehearsal of the N > 1 path (SEG_BENCH_BACKEND=gloo: RCCL does not share a device)
     ndev = torch.cuda.device_count()
+    if local >= ndev and backend == "nccl":
+        raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} visible GPU(s): one rank per GPU "
+                           "(SEG_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs)")
     local_dev = local % ndev if ndev else local
+    shared_device = world > max(ndev, 1)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    backend = os.environ.get("SEG_BENCH_BACKEND", "nccl")
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -463,6 +548,10 @@ def main():
                     "step": step_roof,
                     "max_layer": r["max_layer"]}
         ctx.profile(False)
+        if shared_device:
+            # ranks time-slicing one GPU: per-kernel times include the other ranks' kernels
+            roofline = {"invalid": f"{world} ranks share {ndev} GPU(s) (rehearsal): kernel times "
+                                   "include other ranks' work", "bound": "mfma", "frac": None}
 
     # training-summary mIoU of the metric (define_metrics.py:5-20 via the device confusion
     # kernel), on the strong images of one extra forward + loss with fused decisions, outside
@@ -507,12 +596,22 @@ def main():
     ctx.close()
     train_py = None
     if world == 1 and not args.no_train_py and args.config == "C2":
-        train_py = train_py_leg(args)
-        train_py["ratio_to_value"] = round(train_py["images_per_sec"] / (NB * args.steps / elapsed), 3)
+        # a failure of this side leg (host PNG encode, TFRecord writes, decode threads, a second
+        # context) must not cost the headline line
+        try:
+            train_py = train_py_leg(args)
+            train_py["ratio_to_value"] = round(train_py["images_per_sec"] /
+                                               (NB * args.steps / elapsed), 3)
+        except Exception as e:   # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            train_py = {"error": repr(e)[:500]}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C2":
         cpu = cpu_baseline(pyramid=args.pyramid)
 
+    if world > 1 and comm["world_size"] != args.gpus:
+        raise RuntimeError(f"process group has {comm['world_size']} ranks, --gpus {args.gpus}")
     if rank == 0:
         value = world * NB * args.steps / elapsed
         out = {"metric": "training images/sec at 1024x2048 bf16, 1/2/4/8 MI355X + mIoU vs ref",

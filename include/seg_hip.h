@@ -145,7 +145,11 @@ int seg_confusion(seg_ctx* ctx, const int32_t* labels, const int32_t* decisions,
  * (hierarchical.py:88-130) -> cid_map[n_map] (training -> evaluation/inference cids, -1 =
  * void -> max+1; _map_predictions_to_new_cids :490-522) -> optional _replace_voids
  * (:577-630) -> NEAREST_NEIGHBOR align_corners resize to out_h x out_w (_resize_predictions
- * :524-575). decisions_out: device int32 [N][out_h][out_w]. */
+ * :524-575). decisions_out: device int32 [N][out_h][out_w].
+ * replace_voids: 0 = none; 1 = the EVAL order above (replace at network resolution, then the
+ * nearest resize); 2 = the PREDICT order (:227-231): nearest-resize the decisions and
+ * ResizeBilinear(align_corners) the l1 probabilities to out_h x out_w first, then replace
+ * voids from the top-2 of the RESIZED probabilities. 1 and 2 agree when out = network size. */
 int seg_set_bn_inference(seg_ctx* ctx, int on);
 int seg_predict(seg_ctx* ctx, const int32_t* cid_map, int n_map, int replace_voids, int out_h,
                 int out_w, int32_t* decisions_out, void* stream);

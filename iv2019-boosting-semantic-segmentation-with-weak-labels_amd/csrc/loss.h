@@ -44,7 +44,7 @@ struct EvalArgs {
   int N, Hl, Wl, ldl;
   int H, W;                // network resolution (where decisions are formed)
   int Ho, Wo;              // output (label) resolution
-  int replace_voids;
+  int replace_voids;       // 0 no, 1 EVAL order (replace, then resize), 2 PREDICT order
   int n_map;               // entries of map (= training classes)
   int map[SEG_MAX_PP];     // training cid -> new cid (voids already replaced)
   int* out;                // [N][Ho][Wo]

@@ -496,7 +496,55 @@ __global__ __launch_bounds__(256) void eval_decisions_kernel(EvalArgs a, LossTab
       d = t.l1_to_common[d1];
     }
     d = a.map[d];   // tf.gather(ocids2ncids, decs)
-    if (a.replace_voids) {
+    if (a.replace_voids == 2) {
+      // PREDICT order (define_estimator_hierarchical.py:227-231): _resize_predictions first --
+      // decisions NEAREST (above), l1_probabilities ResizeBilinear(align_corners) from the
+      // network to the output size -- then _replace_voids on the RESIZED probabilities
+      // (top_k(k=2), stable; void = decision C1 - 1). The 4 network-resolution pixels of the
+      // output pixel's footprint get their l1 softmax from the low-res logits as above.
+      int y0, y1, x0, x1;
+      float ylp, xlp;
+      lerp_of(yo, a.H, a.Ho, y0, y1, ylp);
+      lerp_of(xo, a.W, a.Wo, x0, x1, xlp);
+      float q[4][C1];
+      const int ys[2] = {y0, y1}, xs[2] = {x0, x1};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int ya, yb, xa, xb;
+        float ly, lx;
+        lerp_of(ys[k >> 1], a.Hl, a.H, ya, yb, ly);
+        lerp_of(xs[k & 1], a.Wl, a.W, xa, xb, lx);
+        const float* ta = base + ((size_t)ya * a.Wl + xa) * a.ldl;
+        const float* tb = base + ((size_t)ya * a.Wl + xb) * a.ldl;
+        const float* ba = base + ((size_t)yb * a.Wl + xa) * a.ldl;
+        const float* bb = base + ((size_t)yb * a.Wl + xb) * a.ldl;
+        float m = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < C1; ++c) {
+          float top = ta[c] + (tb[c] - ta[c]) * lx;
+          float bot = ba[c] + (bb[c] - ba[c]) * lx;
+          q[k][c] = top + (bot - top) * ly;
+          m = fmaxf(m, q[k][c]);
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < C1; ++c) { q[k][c] = __expf(q[k][c] - m); s += q[k][c]; }
+        const float rs = 1.f / s;
+#pragma unroll
+        for (int c = 0; c < C1; ++c) q[k][c] = q[k][c] * rs;
+      }
+      int i1 = -1, i2 = -1;
+      float v1 = 0.f, v2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < C1; ++c) {
+        const float top = q[0][c] + (q[1][c] - q[0][c]) * xlp;
+        const float bot = q[2][c] + (q[3][c] - q[2][c]) * xlp;
+        const float v = top + (bot - top) * ylp;
+        if (i1 < 0 || v > v1) { i2 = i1; v2 = v1; i1 = c; v1 = v; }
+        else if (i2 < 0 || v > v2) { i2 = c; v2 = v; }
+      }
+      d = d == C1 - 1 ? i2 : i1;
+    } else if (a.replace_voids) {
       // top_k(l1_probabilities, 2) (stable: equal values keep the lower index first);
       // l1_probabilities keep C1 channels (the segment-sum remap does not apply to them)
       int d2 = -1;

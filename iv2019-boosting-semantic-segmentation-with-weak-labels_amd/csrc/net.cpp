@@ -1752,10 +1752,12 @@ int seg_predict(seg_ctx* c, const int32_t* cid_map, int n_map, int replace_voids
     return set_err(&c->err, -EINVAL, "cid map has %d entries, the model has %d training classes",
                    n_map, c->tables.n_pp);
   if (out_h < 1 || out_w < 1) return set_err(&c->err, -EINVAL, "bad output size %dx%d", out_h, out_w);
+  if (replace_voids < 0 || replace_voids > 2)
+    return set_err(&c->err, -EINVAL, "replace_voids = %d (0, 1 or 2)", replace_voids);
   EvalArgs a{};
   a.logits = c->head_in; a.N = c->logits.N; a.Hl = c->logits.H; a.Wl = c->logits.W;
   a.ldl = c->ldl; a.H = g.height; a.W = g.width; a.Ho = out_h; a.Wo = out_w;
-  a.replace_voids = replace_voids ? 1 : 0; a.n_map = n_map; a.out = decisions_out;
+  a.replace_voids = replace_voids; a.n_map = n_map; a.out = decisions_out;
   int mx = -1;
   for (int i = 0; i < n_map; ++i) mx = std::max(mx, (int)cid_map[i]);
   for (int i = 0; i < n_map; ++i) {   // utils._replacevoids: -1 -> max + 1

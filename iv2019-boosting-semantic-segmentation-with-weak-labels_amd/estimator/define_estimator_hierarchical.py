@@ -163,10 +163,11 @@ def _predict_spec(predictions, features, params):
     """PREDICT branch (define_estimator_hierarchical.py:203-238): decisions in TRAINING cids
     (the reference leaves the inference-cid mapping commented out, :226-227), resized to
     (height_system, width_system) when both are set, else to the raw image size, else kept at
-    network resolution (_resize_predictions, nearest align-corners); --replace_voids runs on
-    the device only where that resize is the identity (the reference replaces voids on
-    bilinearly resized probabilities). The full-resolution logits / probabilities / per-head
-    decisions stay lazy entries of the model's predictions (materialised on first access)."""
+    network resolution (_resize_predictions: decisions nearest align-corners, l1 probabilities
+    bilinear align-corners); --replace_voids then takes the top-2 of the RESIZED l1
+    probabilities (_replace_voids, :530-630), all in one device launch. The full-resolution
+    logits / probabilities / per-head decisions stay lazy entries of the model's predictions
+    (materialised on first access)."""
     import torch
     ctx = predictions['_context']
     img = features['proimages']
@@ -176,11 +177,8 @@ def _predict_spec(predictions, features, params):
         raw = features.get('rawimages')
         size = (int(raw.shape[1]), int(raw.shape[2])) if raw is not None else (h_net, w_net)
     replace = bool(getattr(params, 'replace_voids', False))
-    if replace and tuple(size) != (h_net, w_net):
-        raise NotImplementedError('replace_voids with a prediction size different from the '
-                                  'network size (bilinear probability resize) is not built')
     decs = torch.empty((n,) + tuple(size), dtype=torch.int32, device=img.device)
-    ctx.predict(list(range(params.output_Nclasses)), decs, replace_voids=replace)
+    ctx.predict(list(range(params.output_Nclasses)), decs, replace_voids=replace, order="predict")
     out = predictions
     out['decisions'] = decs
     for k in ('rawimages', 'rawimagespaths'):

@@ -255,17 +255,23 @@ class SegContext:
         check(LIB.seg_set_bn_inference(self.h, 1 if on else 0), self.h)
         self.bn_inference = bool(on)
 
-    def predict(self, cid_map, out, replace_voids=False, stream=None):
+    def predict(self, cid_map, out, replace_voids=False, stream=None, order="eval"):
         """Decisions of the last forward mapped through ``cid_map`` (training -> eval/inference
         cids, -1 = void), optionally void-replaced, nearest-neighbour resized to out's
-        [N, Ho, Wo] (device int32)."""
+        [N, Ho, Wo] (device int32). ``order``: "eval" replaces voids at network resolution
+        before the resize (the EVAL branch); "predict" resizes first -- l1 probabilities
+        bilinearly (align_corners) -- and replaces voids on the resized probabilities (the
+        PREDICT branch, define_estimator_hierarchical.py:227-231)."""
+        if order not in ("eval", "predict"):
+            raise ValueError(f"order must be 'eval' or 'predict', got {order!r}")
         m = (ctypes.c_int32 * len(cid_map))(*[int(v) for v in cid_map])
         import torch
         n = self.cfg.nb_pp + self.cfg.nb_pb + self.cfg.nb_pi
         if not (out.dtype == torch.int32 and out.dim() == 3 and out.is_contiguous()
                 and out.shape[0] == n and out.is_cuda):
             raise ValueError(f"decisions buffer must be a contiguous device int32 [{n}, Ho, Wo]")
-        check(LIB.seg_predict(self.h, m, len(cid_map), 1 if replace_voids else 0,
+        rv = (2 if order == "predict" else 1) if replace_voids else 0
+        check(LIB.seg_predict(self.h, m, len(cid_map), rv,
                               int(out.shape[1]), int(out.shape[2]), _ptr(out), _stream(stream)),
               self.h)
 

@@ -41,29 +41,38 @@ def synthetic_seed(rank, step):
 def synthetic_train_input(config, params):
     """Endless seeded batches shaped like the heterogeneous-supervision pipeline, per rank.
 
-    The first ``--synthetic_pool`` batches (seeds synthetic_seed(rank, k)) are generated on
-    the host once and stay resident in HBM; later steps cycle through them. Regenerating
-    every step would cost the host ~0.1 GB of images + 126 MB of soft labels per weak image
-    at 1024 x 2048 plus the H2D copies, far more than the device step."""
+    With ``--synthetic_pool`` k > 0 (default 8) the first k batches (seeds synthetic_seed(rank,
+    j)) are generated on the host once and stay resident in HBM; later steps cycle through them
+    (the same tensors again: nothing downstream writes its input in place). Regenerating every
+    step would cost the host ~0.1 GB of images + 126 MB of soft labels per weak image at
+    1024 x 2048 plus the H2D copies, far more than the device step. k = 0 generates a fresh
+    seeded batch every step (seed synthetic_seed(rank, step))."""
     import torch
     from input_pipelines.synthetic import batch
     rank = int(os.environ.get('RANK', 0))
     nb = rank_sub_batches(config, params)
     dev = torch.device('cuda', torch.cuda.current_device())
-    pool_n = max(1, int(getattr(params, 'synthetic_pool', 8) or 1))
+    pool_n = int(getattr(params, 'synthetic_pool', 8) or 0)
+    if pool_n < 0:
+        raise ValueError(f"--synthetic_pool must be >= 0, got {pool_n}")
+
+    def make(step):
+        b = batch(synthetic_seed(rank, step), *nb, params.height_feature_extractor,
+                  params.width_feature_extractor)
+        pin = lambda a: torch.from_numpy(a).pin_memory().to(dev, non_blocking=True)
+        return ({'proimages': pin(b['images'])},
+                {'prolabels_per_pixel': pin(b['px']),
+                 'prolabels_per_bbox': pin(b['bbox']) if nb[1] else None,
+                 'prolabels_per_image': pin(b['tag']) if nb[2] else None})
     pool = []
     step = 0
     while True:
-        if len(pool) < pool_n:
-            b = batch(synthetic_seed(rank, step), *nb, params.height_feature_extractor,
-                      params.width_feature_extractor)
-            pin = lambda a: torch.from_numpy(a).pin_memory().to(dev, non_blocking=True)
-            pool.append(({'proimages': pin(b['images'])},
-                         {'prolabels_per_pixel': pin(b['px']),
-                          'prolabels_per_bbox': pin(b['bbox']) if nb[1] else None,
-                          'prolabels_per_image': pin(b['tag']) if nb[2] else None}))
-            del b
-        yield pool[step % pool_n]
+        if pool_n == 0:
+            yield make(step)
+        else:
+            if len(pool) < pool_n:
+                pool.append(make(step))
+            yield pool[step % pool_n]
         step += 1
 
 
@@ -84,7 +93,8 @@ def add_train_input_pipeline_arguments(argparser):
     argparser.add_argument('--input_prefetch', type=int, default=2,
                            help='real-data batches decoded ahead of the training step')
     argparser.add_argument('--synthetic_pool', type=int, default=8,
-                           help='synthetic input: seeded batches kept resident in HBM and cycled')
+                           help='synthetic input: number of seeded batches kept resident in HBM '
+                                'and cycled (default 8); 0 = a fresh seeded batch every step')
     argparser.add_argument('--input_seed', type=int, default=0,
                            help='seed of the shuffles and crop offsets (the reference seeds nothing)')
 

@@ -593,6 +593,25 @@ class OracleNet:
         wx = nearest_ac_index(self.cfg.width, out_w)
         return d[:, hy][:, :, wx]
 
+    def predict_decisions(self, low, out_h, out_w, replace_voids=False):
+        """PREDICT branch (define_estimator_hierarchical.py:203-232): the fused decisions in
+        training cids (the cid mapping is commented out, :226-227) and the l1 probabilities go
+        through _resize_predictions (:530-575: decisions NEAREST_NEIGHBOR align_corners, l1
+        probabilities ResizeBilinear align_corners) and THEN _replace_voids (:577-630) on the
+        resized probabilities: void = decision C1 - 1 -> the second of top_k(k=2), else the
+        first (the reference's tf.equal "assertion" is not an assert: the first index replaces
+        the decision everywhere else). Returns int64 [N, out_h, out_w]."""
+        _, probs, _, fused = self.head_predictions(low)
+        hy = nearest_ac_index(self.cfg.height, out_h)
+        wx = nearest_ac_index(self.cfg.width, out_w)
+        d = fused[:, hy][:, :, wx]
+        if replace_voids:
+            p1 = resize_bilinear_ac(probs["l1_logits"], out_h, out_w)   # [N, C1, Ho, Wo]
+            c1 = p1.shape[1]
+            order = torch.sort(-p1, dim=1, stable=True).indices
+            d = torch.where(d == c1 - 1, order[:, 1], order[:, 0])
+        return d
+
     # -- losses (define_losses_hierarchical.py:98-210) ---------------------------------
     def losses(self, low, px_labels, bbox_soft=None, tag_soft=None, weak_l1_decisions=None):
         """`weak_l1_decisions` (int [Nb_pb + Nb_pi, H, W], optional) replaces this forward's

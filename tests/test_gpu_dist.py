@@ -248,13 +248,22 @@ def test_four_ranks_mixed_batch_matches_oracle(tmp_path):
     cfg = SegConfig(height=DP4_H, width=DP4_W, nb_pp=1, nb_pb=2, nb_pi=1, pyramid="none")
     p0 = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=0).items()}
 
+    from tests.test_gpu_train import _gate_flips
+    flips = []
+
+    from test_gpu_train import _gate_flips   # tests/ is on sys.path (pytest's prepend mode)
+    flips = []
+
     def oracle(dtype):
         losses, counts, grads, stats = [], [], [], []
         for r in range(DP4_WORLD):
             d = batch(1000003 * r, 1, 2, 1, DP4_H, DP4_W)   # train.synthetic_train_input, rank r
             net = OracleNet(cfg, {k: v.astype(np.float64) for k, v in p0.items()}, dtype=dtype)
-            L, _, g, _, _, _, st = net.train_step(d["images"], d["px"], d["bbox"], d["tag"],
-                                                  lr=1e-3, weak_l1_decisions=res[r][1][0][3])
+            L, low, g, _, _, _, st = net.train_step(d["images"], d["px"], d["bbox"], d["tag"],
+                                                    lr=1e-3, weak_l1_decisions=res[r][1][0][3])
+            if dtype == torch.float64:   # the oracle's own l1 gate vs the native rank's
+                flips.append(_gate_flips(net, {q_: v.detach() for q_, v in low.items()},
+                                         np.concatenate([d["bbox"], d["tag"]]), res[r][1][0][3], 1))
             losses.append([float(L[n]) for n in ("segmentation", "l1_segmentation",
                                                   "l2_vehicle_segmentation", "l2_human_segmentation")])
             counts.append(tuple(int(c) for c in L["counts"]))
@@ -273,6 +282,13 @@ def test_four_ranks_mixed_batch_matches_oracle(tmp_path):
     for r in range(DP4_WORLD):
         np.testing.assert_allclose(res[r][1][0][1], ref_l[r], rtol=1e-3, atol=1e-6, err_msg=f"rank {r}")
         assert tuple(res[r][1][0][2]) == ref_c[r], (r, res[r][1][0][2], ref_c[r])
+    # the weak-weight gate itself (as test_gpu_train): the oracle's own l1 argmax moves at most
+    # 0.1 % of a weak image's pixels in or out of a head's weights on every rank
+    assert all(int(f.max()) <= max(2, DP4_H * DP4_W // 1000) for f in flips), flips
+    # the weak-weight gate itself (as test_gpu_train): the oracle's own l1 argmax moves at most
+    # 0.1 % of a weak image's pixels in or out of a head's weights on every rank
+    assert len(flips) == DP4_WORLD
+    assert all(int(f.max()) <= max(2, DP4_H * DP4_W // 1000) for f in flips), flips
     # per-rank normalisation is not the global one: the ranks' counts differ
     assert len(set(ref_c)) > 1
 

@@ -129,6 +129,81 @@ def test_predict_decisions(cuda, mapname, out_hw, replace_voids):
     ctx.close()
 
 
+@pytest.mark.parametrize("out_hw", [(64, 128), (32, 64), (128, 256), (45, 77), (97, 301)])
+def test_predict_order_resize_then_replace_voids(cuda, out_hw):
+    """the PREDICT branch resizes first -- decisions nearest, l1
+    probabilities bilinear (align_corners) -- and replaces voids on the RESIZED probabilities
+    (define_estimator_hierarchical.py:227-231, :530-630), against
+    OracleNet.predict_decisions on the native low-res logits. At the network size it equals
+    the EVAL order (same launch, mode 1). Only fp32-vs-fp32 rounding near-ties of the top-2
+    may differ (<= 1e-3 of the pixels)."""
+    from input_pipelines.synthetic import batch
+    cfg = CFGS[0]
+    params = _params_with_moving_stats(cfg)
+    data = batch(12, cfg.nb, 0, 0, cfg.height, cfg.width)
+    ctx = _ctx(cfg)
+    ctx.load_params(params)
+    ctx.set_bn_inference(True)
+    ctx.forward(torch.as_tensor(data["images"]).to(cuda))
+    _, _, lg = ctx.outputs()
+    low = lg.cpu().permute(0, 3, 1, 2).contiguous()
+    c1, c2 = 14, 7
+    net = OracleNet(cfg, params, dtype=torch.float32)
+    lowd = {"l1_logits": low[:, :c1], "l2_vehicle_logits": low[:, c1:c1 + c2],
+            "l2_human_logits": low[:, c1 + c2:c1 + c2 + 3]}
+    ident = list(range(20))   # PREDICT keeps training cids
+    got = {}
+    for rv in (False, True):
+        out = torch.full((cfg.nb,) + out_hw, -7, dtype=torch.int32, device=cuda)
+        ctx.predict(ident, out, replace_voids=rv, order="predict")
+        nat = out.cpu().numpy()
+        ref = net.predict_decisions(lowd, out_hw[0], out_hw[1], replace_voids=rv).numpy()
+        assert nat.shape == ref.shape and (nat >= 0).all()
+        assert float(np.mean(nat != ref)) <= 1e-3, (rv, float(np.mean(nat != ref)))
+        got[rv] = nat
+    # replace_voids changes something (the void class of l1 and the l1-argmax elsewhere)
+    assert np.any(got[True] != got[False])
+    if out_hw == (cfg.height, cfg.width):
+        out = torch.empty((cfg.nb,) + out_hw, dtype=torch.int32, device=cuda)
+        ctx.predict(ident, out, replace_voids=True, order="eval")
+        np.testing.assert_array_equal(out.cpu().numpy(), got[True])
+    ctx.close()
+
+
+def test_predict_spec_replace_voids_resized(cuda, tmp_path, init_ckpt):
+    """define_estimator(PREDICT) with --replace_voids and a system size different from the
+    network size (was NotImplementedError in round 4): the facade's decisions equal
+    OracleNet.predict_decisions on the same forward's logits."""
+    from estimator.define_estimator_hierarchical import define_estimator
+    from estimator.mode_keys import ModeKeys
+    from models.resnet50_extended_model_hierarchical import add_model_arguments, model
+    from system_factory import RunConfig
+    from utils.utils import SemanticSegmentationArguments
+    from input_pipelines.synthetic import batch
+    a = SemanticSegmentationArguments(mode=ModeKeys.PREDICT)
+    add_model_arguments(a.argparser)
+    s = a.parse_args([str(tmp_path), PROBLEM, str(tmp_path / "pred"), "--Nb", "1",
+                      "--height_feature_extractor", "48", "--width_feature_extractor", "64",
+                      "--compute_dtype", "fp32", "--replace_voids"])
+    s.per_pixel_dataset_name = "cityscapes"
+    s.height_system, s.width_system = 100, 150
+    params = init_ckpt(tmp_path, pyramid="none", height=48, width=64, nb_pp=1, dtype="fp32")
+    data = batch(5, 1, 0, 0, 48, 64)
+    feats = {"proimages": torch.as_tensor(data["images"]).to(cuda)}
+    spec = define_estimator(ModeKeys.PREDICT, feats, None, model, RunConfig(), s)
+    d = spec.predictions["decisions"].cpu().numpy()
+    assert d.shape == (1, 100, 150)
+    ctx = spec.predictions["_context"]
+    _, _, lg = ctx.outputs()
+    low = lg.cpu().permute(0, 3, 1, 2).contiguous()
+    cfg = SegConfig(height=48, width=64, nb_pp=1, pyramid="none")
+    net = OracleNet(cfg, {k: v.numpy() for k, v in params.items()}, dtype=torch.float32)
+    lowd = {"l1_logits": low[:, :14], "l2_vehicle_logits": low[:, 14:21],
+            "l2_human_logits": low[:, 21:24]}
+    ref = net.predict_decisions(lowd, 100, 150, replace_voids=True).numpy()
+    assert float(np.mean(d != ref)) <= 1e-3
+
+
 def test_predict_rejects_bad_map(cuda):
     cfg = CFGS[0]
     ctx = _ctx(cfg)

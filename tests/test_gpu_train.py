@@ -33,8 +33,8 @@ under that mask must equal the native counts exactly (proof that the captured de
 the loss head's own), and the oracle's own gate may differ from the native one on at most
 0.1 % of a weak image's pixels per head (the flip count, asserted separately).
 
-Tolerances: per-step losses 1e-3, all four terms (the log line prints 4 decimals: 5e-4
-absolute on top);
+Tolerances: per-step losses at rtol 1e-3 with no absolute slack, all four terms, read from
+the device after each step's train_op (fp32 scalars, not the 4-decimal log line);
 the parameter, momentum and EMA changes over the three steps (w3 - w0, v3, e3 - w0, all
 trainable tensors flattened, L2-relative) max(1e-2, 3 x the fp32 oracle's own gap on the same
 quantity); BN moving statistics max(1e-3, 4 x that gap).
@@ -71,6 +71,29 @@ def _capture_weak_decisions(monkeypatch, captured):
         captured.append((d1, L.counts()))
         return L
     monkeypatch.setattr(deh, "define_losses", wrapped)
+
+
+def _capture_device_losses(monkeypatch, out):
+    """Wrap the facade's define_estimator so that, right after each TRAIN step's train_op
+    (define_estimator_hierarchical.py:120-129: the regulariser -- and so 'total' -- is written
+    by the fused update), the four logged loss terms are read from the device as fp32 scalars
+    (the same values the log line prints to 4 decimals)."""
+    import system_factory as sf
+    orig = sf.define_estimator
+
+    def wrapped(mode, features, labels, model_fn, config, params):
+        spec = orig(mode, features, labels, model_fn, config, params)
+        if spec.train_op is None:
+            return spec
+
+        def train_op():
+            L = spec.train_op()
+            out.append(tuple(float(L[n]) for n in ("total", "l1_segmentation",
+                                                   "l2_vehicle_segmentation",
+                                                   "l2_human_segmentation")))
+            return L
+        return spec._replace(train_op=train_op)
+    monkeypatch.setattr(sf, "define_estimator", wrapped)
 
 
 def _gate_flips(net, low, weak, native_d1, npp):
@@ -110,13 +133,15 @@ def test_train_main_matches_oracle_trajectory(cuda, tmp_path, capsys, monkeypatc
             "--save_summaries_steps", "1", "--save_checkpoints_steps", "100"]
     if nesterov:   # MomentumOptimizer(use_nesterov=True), define_optimizer.py:17-20
         argv.append("--use_nesterov")
-    native = []
+    native, logged = [], []
     _capture_weak_decisions(monkeypatch, native)
+    _capture_device_losses(monkeypatch, logged)
     assert train.main(argv) == 3 and len(native) == 3
     out = capsys.readouterr().out
-    logged = [tuple(float(v) for v in m) for m in
-              re.findall(r"step \d+: total ([-\d.]+) l1 ([-\d.]+) l2v ([-\d.]+) l2h ([-\d.]+)", out)]
-    assert len(logged) == 3, out
+    printed = re.findall(r"step \d+: total ([-\d.]+) l1 ([-\d.]+) l2v ([-\d.]+) l2h ([-\d.]+)", out)
+    assert len(logged) == 3 and len(printed) == 3, out
+    # the log line is the device value rounded to 4 decimals
+    assert all(abs(float(p[0]) - g[0]) <= 5.1e-5 for p, g in zip(printed, logged)), (printed, logged)
     ctx = next(iter(mh._CONTEXTS.values()))
     assert ctx.ema is not None   # ema_decay defaults to 0.9 (utils/utils.py:112)
 
@@ -154,7 +179,7 @@ def test_train_main_matches_oracle_trajectory(cuda, tmp_path, capsys, monkeypatc
     # every term at 1e-3: with weak images both chains use the native weak-weight mask
     for k, (got, ref) in enumerate(zip(logged, ref_losses)):
         got, ref = np.array(got), np.array(ref)
-        assert np.all(np.abs(got - ref) <= 1e-3 * np.abs(ref) + 5e-4), (k, got, ref, l32[k])
+        assert np.all(np.abs(got - ref) <= 1e-3 * np.abs(ref)), (k, got, ref, l32[k])
     # the gate itself, counted separately: the oracle's own argmax moves at most 0.1 % of a
     # weak image's pixels in or out of a head's weights (measured: <= 1 px at step 0, where
     # both start from the same weights; <= 4 of 8192 px at steps 1-2, where the trajectories
@@ -250,8 +275,9 @@ def test_train_main_real_data_matches_oracle(cuda, tmp_path, capsys, monkeypatch
             yield feats, labels
     monkeypatch.setattr(train_inputs, "heterogeneous_train_input", capture)
     monkeypatch.setattr(tfrecords, "prepare_images_crop", crop)
-    native = []
+    native, logged = [], []
     _capture_weak_decisions(monkeypatch, native)
+    _capture_device_losses(monkeypatch, logged)
     argv = [str(tmp_path / "logs"), "cityscapes", "--max_steps", "2", "--compute_dtype", "fp32",
             "--height_feature_extractor", str(H), "--width_feature_extractor", str(W),
             "--Nb_per_pixel", "2", "--Nb_per_bbox", "1", "--Nb_per_image", "1",
@@ -265,8 +291,6 @@ def test_train_main_real_data_matches_oracle(cuda, tmp_path, capsys, monkeypatch
             "--input_workers", "3", "--input_prefetch", "2"]
     assert train.main(argv) == 2
     out = capsys.readouterr().out
-    logged = [tuple(float(v) for v in m) for m in
-              re.findall(r"step \d+: total ([-\d.]+) l1 ([-\d.]+) l2v ([-\d.]+) l2h ([-\d.]+)", out)]
     assert len(logged) == 2 and len(captured) >= 2, out
     ctx = next(iter(mh._CONTEXTS.values()))
     # the per-pixel labels are training cids (void = 19) and the crop path is bit-exact
@@ -307,7 +331,7 @@ def test_train_main_real_data_matches_oracle(cuda, tmp_path, capsys, monkeypatch
     l32, p32, m32, e32, _ = chain(torch.float32)
     for k, (got, ref) in enumerate(zip(logged, ref_losses)):
         got, ref = np.array(got), np.array(ref)
-        assert np.all(np.abs(got - ref) <= 1e-3 * np.abs(ref) + 5e-4), (k, got, ref, l32[k])
+        assert np.all(np.abs(got - ref) <= 1e-3 * np.abs(ref)), (k, got, ref, l32[k])
     assert all(int(f.max()) <= max(2, H * W // 1000) for f in flips), flips
     nat_p, nat_m, nat_e = ctx.named("params"), ctx.named("momentum"), ctx.named("ema")
     keys = list(ref_m)
@@ -321,4 +345,94 @@ def test_train_main_real_data_matches_oracle(cuda, tmp_path, capsys, monkeypatch
         rows.append((what, err, gap))
     assert all(err < max(1e-2, 3 * gap) for _, err, gap in rows), rows
     assert json.load(open(os.path.join(tiny, "tags.json")))
+    mh.release_contexts()
+
+
+@pytest.mark.timeout(600)
+def test_train_main_c1_reference_default_shape(cuda, tmp_path, monkeypatch):
+    """BASELINE config C1 -- the reference train.py's own Cityscapes default
+    (code/train.py:55-64: ResNet-50, no pyramid module, 512 x 1024, batch 2 per-pixel images,
+    Nb_per_bbox = Nb_per_image = 0), fp32 (the reference's arithmetic), through ``train.main``
+    for one step at the default learning rate 0.01 and EMA 0.9, against OracleNet.train_step in
+    float64 on the same seeded batch (train.synthetic_train_input's seed for rank 0, step 0).
+
+    Tolerances: loss terms at rtol 1e-3 (device fp32 values, no absolute slack) and the
+    non-zero-weight counts exact; the low-resolution logits (64 x 128) L2-relative max(1e-3,
+    4 x the fp32 oracle's own gap); the parameter change w1 - w0, the momentum and the EMA change
+    max(1e-2, 3 x that gap) (the trajectory tests' bound); BN moving statistics max(1e-3, 4 x gap).
+    At 512 x 1024 every BN channel of the encoder averages >= 16k samples, so the conditioning
+    problem of the small step tests (module docstring of test_gpu_step.py) is much weaker here."""
+    import train
+    from estimator.define_estimator_hierarchical import get_or_create_global_step
+    from input_pipelines.synthetic import batch
+    from models import resnet50_extended_model_hierarchical as mh
+    mh.release_contexts()
+    get_or_create_global_step().value = 0
+    H, W, NPP = 512, 1024, 2
+    argv = [str(tmp_path / "logs"), "cityscapes", "--max_steps", "1", "--compute_dtype", "fp32",
+            "--height_feature_extractor", str(H), "--width_feature_extractor", str(W),
+            "--Nb_per_pixel", str(NPP), "--Nb_per_bbox", "0", "--Nb_per_image", "0",
+            "--synthetic_pool", "1", "--save_summaries_steps", "1", "--save_checkpoints_steps", "100"]
+    import estimator.define_estimator_hierarchical as deh
+    orig = deh.define_losses
+    seen, logged = [], []
+
+    def wrapped(mode, predictions, labels, config, params):
+        L = orig(mode, predictions, labels, config, params)
+        ctx = predictions['_context']
+        seen.append((ctx.outputs()[2].cpu().numpy().copy(), L.counts(),
+                     float(params.learning_rate_initial)))
+        return L
+    monkeypatch.setattr(deh, "define_losses", wrapped)
+    _capture_device_losses(monkeypatch, logged)
+    assert train.main(argv) == 1 and len(seen) == 1 and len(logged) == 1
+    ctx = next(iter(mh._CONTEXTS.values()))
+    assert (ctx.cfg.depth, ctx.cfg.pyramid, ctx.cfg.height, ctx.cfg.width, ctx.cfg.nb_pp) == \
+        (50, "none", H, W, NPP)
+    logits, counts, lr = seen[0]
+    assert lr == 0.01
+    nat_p, nat_m, nat_e = ctx.named("params"), ctx.named("momentum"), ctx.named("ema")
+
+    cfg = SegConfig(height=H, width=W, nb_pp=NPP, pyramid="none")
+    p0 = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=0).items()}
+    d = batch(0, NPP, 0, 0, H, W)
+
+    def step(dtype):
+        net = OracleNet(cfg, {k: v.astype(np.float64) for k, v in p0.items()}, dtype=dtype)
+        L, low, _, new_p, mom, ema, _ = net.train_step(d["images"], d["px"], lr=lr, ema_decay=0.9,
+                                                       step=0)
+        out = (tuple(float(L[n].detach()) for n in ("total", "l1_segmentation",
+                                                   "l2_vehicle_segmentation", "l2_human_segmentation")),
+               tuple(int(c) for c in L["counts"]),
+               {q: v.detach().permute(0, 2, 3, 1).numpy() for q, v in low.items()},
+               {n: v.detach().numpy() for n, v in new_p.items()},
+               {n: v.numpy() for n, v in mom.items()}, {n: v.detach().numpy() for n, v in ema.items()})
+        del net, L, low
+        return out
+
+    ref_l, ref_c, ref_low, ref_p, ref_m, ref_e = step(torch.float64)
+    l32, _, low32, p32, m32, e32 = step(torch.float32)
+    got = np.array(logged[0])
+    assert np.all(np.abs(got - np.array(ref_l)) <= 1e-3 * np.abs(np.array(ref_l))), (got, ref_l, l32)
+    assert counts == ref_c, (counts, ref_c)
+    c1, c2 = 14, 7
+    for key, a, b in (("l1_logits", 0, c1), ("l2_vehicle_logits", c1, c1 + c2),
+                      ("l2_human_logits", c1 + c2, c1 + c2 + 3)):
+        gap = _rel(low32[key], ref_low[key])
+        err = _rel(logits[..., a:b], ref_low[key])
+        assert err < max(1e-3, 4 * gap), (key, err, gap)
+    keys = list(ref_m)
+    flat = lambda dd, ks: np.concatenate([np.asarray(dd[k], np.float64).reshape(-1) for k in ks])
+    w0 = flat(p0, keys)
+    rows = []
+    for what, nat, ref, r32, base in (("momentum", nat_m, ref_m, m32, 0), ("w1 - w0", nat_p, ref_p, p32, w0),
+                                      ("ema - w0", nat_e, ref_e, e32, w0)):
+        gap = _rel(flat(r32, keys) - base, flat(ref, keys) - base)
+        err = _rel(flat(nat, keys) - base, flat(ref, keys) - base)
+        rows.append((what, err, gap))
+    assert all(err < max(1e-2, 3 * gap) for _, err, gap in rows), rows
+    moving = [k for k in ref_p if "moving" in k]
+    gap = _rel(flat(p32, moving), flat(ref_p, moving))
+    assert _rel(flat(nat_p, moving), flat(ref_p, moving)) < max(1e-3, 4 * gap)
+    print("C1 parity:", rows, "losses", got.tolist(), ref_l)
     mh.release_contexts()

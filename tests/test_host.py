@@ -246,3 +246,34 @@ def test_dp_four_ranks_mixed_batch_host_path():
     for r in res:
         assert np.all(np.abs(r[5] - mean) <= bound), float(np.max(np.abs(r[5] - mean) / bound))
         np.testing.assert_array_equal(r[5], res[0][5])
+
+
+def _run_bench(args, env_extra, timeout=300):
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(repo, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout, cwd=repo)
+
+
+def test_bench_world_size_must_match_gpus():
+    """under an external launcher WORLD_SIZE must equal --gpus (a mismatch
+    exits non-zero before anything touches a GPU)."""
+    r = _run_bench(["--gpus", "4", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in r.stderr, r.stderr
+    assert '{"metric"' not in r.stdout
+
+
+def test_bench_launches_ranks_and_propagates_failure():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts two rank processes of itself (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1). Here (no GPU) both ranks fail at device
+    selection: the parent must report the failing rank, print no result line and exit non-zero."""
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {"SEG_BENCH_BACKEND": "nccl"})
+    assert r.returncode != 0
+    assert '{"metric"' not in r.stdout
+    assert "exited with" in r.stderr, r.stderr[-2000:]
+    # each child saw its own rank environment
+    assert "[rank 0]" in r.stderr or "rank 0" in r.stderr

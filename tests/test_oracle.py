@@ -229,6 +229,47 @@ def test_oracle_eval_decisions_map_replace_resize():
     assert (d == CITYSCAPES["veh_to_common"][3]).all()
 
 
+def test_oracle_predict_decisions_resize_then_replace():
+    """predict_decisions (PREDICT order, define_estimator_hierarchical.py:227-231): nearest
+    resize of the fused decisions, bilinear align-corners resize of the l1 probabilities, then
+    _replace_voids on the resized probabilities. Known answers on hand-built logits, and at the
+    network size it equals eval_decisions with the identity map."""
+    import torch
+    from oracle.tfseg import OracleNet, SegConfig, init_params
+    cfg = SegConfig(height=16, width=16, nb_pp=1, pyramid="none")
+    net = OracleNet(cfg, init_params(cfg, seed=0))
+    low = {"l1_logits": torch.zeros(1, 14, 2, 2), "l2_vehicle_logits": torch.zeros(1, 7, 2, 2),
+           "l2_human_logits": torch.zeros(1, 3, 2, 2)}
+    from oracle.tfseg import CITYSCAPES
+    veh = CITYSCAPES["cid_l1_vehicle"]
+    b = list(CITYSCAPES["veh_to_common"]).index(13)   # common cid 13 == C1 - 1 ("void" rule)
+    low["l1_logits"][:, veh] = 4.0         # l1 argmax: the vehicle class ...
+    low["l1_logits"][:, 2] = 3.0           # ... runner-up 2
+    low["l2_vehicle_logits"][:, b] = 1.0   # ... and the vehicle head's class of cid 13
+    ident = list(range(20))
+    assert (net.predict_decisions(low, 7, 9) == 13).all()
+    # void -> second of top-2 of the resized l1 probabilities
+    assert (net.predict_decisions(low, 7, 9, replace_voids=True) == 2).all()
+    low["l2_vehicle_logits"][:, (b + 1) % 7] = 2.0   # another vehicle class wins
+    assert (net.predict_decisions(low, 7, 9) != 13).all()
+    # elsewhere the first of top-2 (the l1 argmax index, not the fused decision)
+    assert (net.predict_decisions(low, 7, 9, replace_voids=True) == veh).all()
+    # left half class 4, right half class 7 at low resolution; the resized probabilities'
+    # top-1 follows the bilinear blend of the two softmaxes, columns split at the midpoint
+    low["l1_logits"].zero_()
+    low["l1_logits"][0, 4, :, 0] = 5.0
+    low["l1_logits"][0, 7, :, 1] = 5.0
+    d = net.predict_decisions(low, 5, 31, replace_voids=True)[0]
+    assert (d[:, :15] == 4).all() and (d[:, 16:] == 7).all()
+    g = torch.Generator().manual_seed(0)
+    low = {k: torch.randn(2, c, 3, 5, generator=g) for k, c in
+           (("l1_logits", 14), ("l2_vehicle_logits", 7), ("l2_human_logits", 3))}
+    for rv in (False, True):
+        a = net.predict_decisions(low, 16, 16, replace_voids=rv)
+        b = net.eval_decisions(low, ident, 16, 16, replace_voids=rv)
+        assert torch.equal(a, b)
+
+
 # ---------------------------------------------------------------- shifted-GEMM conv restatement
 @pytest.mark.parametrize("case", [
     # N, H, W, Ci, Co, k, stride, rate, explicit_pad
