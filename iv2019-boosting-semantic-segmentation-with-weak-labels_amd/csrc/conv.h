@@ -65,8 +65,8 @@ hipError_t launch_weight_flip_batched(int dtype, const FlipJob* jobs, int njobs,
                                       hipStream_t s);
 hipError_t launch_weight_flip_transpose(int dtype, const void* w, void* wt, int co, int kh, int kw,
                                         int ci, hipStream_t s);
-int conv_nt_mtiles(long M);  // upper bound on BN-stat partial tiles (128-row tiles)
-// rows per BN-stat partial tile of the kernel launch_conv_nt will pick (128 or 256)
+int conv_nt_mtiles(long M);  // upper bound on BN-stat partial tiles (64-row tiles)
+// rows per BN-stat partial tile of the kernel launch_conv_nt will pick (64, 128 or 256)
 int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a);
 bool conv_nt_v2_ok(const ConvArgs& a);
 int conv_nt_v2_rows(const ConvArgs& a);   // tile rows (= BN-stat partial rows) of the v2 config
@@ -80,6 +80,10 @@ hipError_t launch_conv_skinny(int dtype, const ConvArgs& a, hipStream_t s);
 // ping-pong 256x256 main loop (conv_pp.hip) for the v2 cases with Co > 128
 bool conv_nt_pp_ok(const ConvArgs& a);
 hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s);
+// short-K dense 1x1 with double-buffered accumulators (conv_db.hip): 256 x 128 tiles, the
+// epilogue of one tile inside the next tile's main loop; BN partials per 64 rows
+bool conv_nt_db_ok(const ConvArgs& a);
+hipError_t launch_conv_nt_db(int dtype, const ConvArgs& a, hipStream_t s);
 // launches that apply ConvArgs::omask: 16-bit dense 1x1 ping-pong with a residual (one tile per
 // workgroup), i.e. the identity units' conv1 data gradient
 bool conv_nt_omask_ok(int dtype, const ConvArgs& a);

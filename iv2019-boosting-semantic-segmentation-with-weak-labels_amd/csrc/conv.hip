@@ -634,7 +634,7 @@ hipError_t wg_dispatch(const WgradArgs& a, hipStream_t s) {
 
 }  // namespace
 
-int conv_nt_mtiles(long M) { return ceil_div(M, 128); }
+int conv_nt_mtiles(long M) { return ceil_div(M, 64); }   // 64-row partials: conv_nt_db
 
 int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a) {
   return (seg_half(dtype) && !out_f32 && conv_nt_v2_ok(a)) ? conv_nt_v2_rows(a) : 128;

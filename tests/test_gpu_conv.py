@@ -27,6 +27,13 @@ CASES = [
     (2, 16, 64, 64, 64, 3, 1, 1, False),      # one 64-channel chunk, Co 64
     (1, 24, 96, 128, 128, 3, 1, 1, False),    # two chunks (second patch streamed), Co 128
     (1, 8, 32, 128, 64, 3, 1, 1, False),      # two chunks, Co 64 (its dgrad: one chunk, Co 128)
+    # short-K dense 1x1, double-buffered accumulators (conv_db.hip: M % 256 == 0, Co % 128 == 0,
+    # 64 <= K <= 512); the dgrad of the same case is a short-K problem too where Ci > 128
+    (2, 16, 32, 256, 512, 1, 1, 1, False),    # K 256 -> 512: 4 x 4 tiles, one per workgroup
+    (1, 16, 16, 64, 256, 1, 1, 1, False),     # K 64: one K-tile per tile
+    (1, 128, 128, 256, 1024, 1, 1, 1, False), # 512 tiles: two per workgroup (epilogue overlapped)
+    (1, 96, 128, 128, 768, 1, 1, 1, False),  # 288 tiles: 2 or 1 per workgroup, K 128
+    (2, 64, 128, 512, 1024, 1, 1, 1, False),  # K 512, 512 tiles; its dgrad K 1024 (ping-pong)
 ]
 
 
@@ -87,7 +94,9 @@ def test_conv_fwd(cuda, dtype, case):
     ldy = Co if Co % 8 == 0 else (Co + 15) // 16 * 16
     yd = torch.zeros((N, Ho, Wo, ldy), dtype=tdt, device=cuda)
     M = N * Ho * Wo
-    stats = torch.zeros(((M + 127) // 128, Co, 2), dtype=torch.float32, device=cuda)
+    # BN partials: one per stat-rows block of the kernel the dispatcher picks (64 / 128 / 256)
+    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], N, H, W, Ci, Ci, Co, Co, k, s, r, int(ep))
+    stats = torch.zeros(((M + tr - 1) // tr, Co, 2), dtype=torch.float32, device=cuda)
     s_ = torch.cuda.current_stream().cuda_stream
     check(LIB.seg_op_conv_fwd(ABI[dtype], xd.data_ptr(), N, H, W, Ci, Ci,
                               wd.data_ptr(), Co, k, s, r, int(ep), yd.data_ptr(), ldy,
@@ -97,7 +106,6 @@ def test_conv_fwd(cuda, dtype, case):
     tol = TOL[dtype]
     assert _rel(y, ref) < tol
     # BN partial statistics: merge (sum, M2 about the tile mean) and compare
-    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], N, H, W, Ci, Ci, Co, Co, k, s, r, int(ep))
     nt = (M + tr - 1) // tr
     st = stats.cpu().numpy().astype(np.float64)[:nt]
     cnt = np.minimum(tr, M - np.arange(nt) * tr).astype(np.float64)

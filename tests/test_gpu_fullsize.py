@@ -126,13 +126,14 @@ def test_conv_c2_layer(cuda, case, dtype):
     M = N * Ho * Wo
     xd, wd = x.to(cuda), w.to(cuda)
     yd = torch.empty((N, Ho, Wo, Co), dtype=TDT[dtype], device=cuda)
-    stats = torch.zeros(((M + 127) // 128, Co, 2), dtype=torch.float32, device=cuda)
+    # BN partials: one per stat-rows block of the kernel the dispatcher picks (64 / 128 / 256)
+    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], N, H, W, Ci, Ci, Co, Co, k, s, r, int(ep))
+    stats = torch.zeros(((M + tr - 1) // tr, Co, 2), dtype=torch.float32, device=cuda)
     check(LIB.seg_op_conv_fwd(ABI[dtype], xd.data_ptr(), N, H, W, Ci, Ci, wd.data_ptr(), Co, k, s, r,
                               int(ep), yd.data_ptr(), Co, stats.data_ptr(), st))
     torch.cuda.synchronize()
     refd = ref.to(cuda)
     _elementwise(yd, refd, 2 * ULP[dtype], 1e-3, f"{name} fwd")
-    tr = LIB.seg_op_conv_stat_rows(ABI[dtype], N, H, W, Ci, Ci, Co, Co, k, s, r, int(ep))
     nt = (M + tr - 1) // tr
     sp = stats[:nt].double()
     cnt = torch.clamp(M - torch.arange(nt, device=cuda) * tr, max=tr).double()

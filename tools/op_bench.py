@@ -19,6 +19,7 @@ SHAPES = {  # N, H, W, Ci, Co, k, stride, rate
     "b1c3": (4, 256, 512, 64, 256, 1, 1, 1),
     "b2c2": (4, 128, 256, 128, 128, 3, 1, 1),
     "b2c1": (4, 128, 256, 512, 128, 1, 1, 1),
+    "b2c3": (4, 128, 256, 128, 512, 1, 1, 1),
 }
 op = sys.argv[1] if len(sys.argv) > 1 else "wgrad"
 N, H, W, Ci, Co, k, s, r = SHAPES[sys.argv[2] if len(sys.argv) > 2 else "b4c2"]
@@ -30,7 +31,7 @@ w = (torch.randn(Co, k, k, Ci, generator=g) * 0.02).to(dev, torch.bfloat16)
 dy = torch.randn(N, H, W, Co, generator=g).to(dev, torch.bfloat16)
 y = torch.empty(N, H, W, Co, device=dev, dtype=torch.bfloat16)
 dx = torch.empty(N, H, W, Ci, device=dev, dtype=torch.bfloat16)
-st = torch.empty((N * H * W + 127) // 128 * Co * 2, device=dev, dtype=torch.float32)
+st = torch.empty((N * H * W + 63) // 64 * Co * 2, device=dev, dtype=torch.float32)   # 64-row partials at most
 dw = torch.empty(Co * k * k * Ci, device=dev, dtype=torch.float32)
 ws = torch.empty(512 << 20, device=dev, dtype=torch.uint8)
 wt = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()

@@ -16,6 +16,8 @@
 #   pmc=OP:LAYER          PMC counter passes of one single-op bench (OP fwd|dgrad|wgrad)
 #   ab=V1,V2,...          interleaved whole-step A/B: the in-tree library vs ab/Vi/libseg_hip.so
 #   ops=V1,V2,...         single-op A/B on the same variants (OPS / LAYERS env override)
+#   envops=VAR            single-op A/B: VAR=0 vs unset (OPS / LAYERS env override)
+#   envab=VAR             interleaved whole-step A/B (benchq): VAR=0 vs unset, REPS rounds
 set -e
 tag=$1; shift
 out=gpurun_out/$tag
@@ -26,7 +28,7 @@ for step in "$@"; do
   echo "== $step" | tee -a "$out/progress.txt"
   case $key in
     suite) timeout -k 10 900 python3 -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > "$out/suite.txt" 2>&1 ;;
-    tests) timeout -k 10 900 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread ${val//,/ } > "$out/tests.txt" 2>&1 ;;
+    tests) timeout -k 10 900 python3 -u -m pytest -x -v --timeout ${TT:-600} --timeout-method thread ${val//,/ } >> "$out/tests.txt" 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.txt" 2>&1 ;;
     bench) timeout -k 10 500 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$out/bench.json" 2> "$out/bench.err" ;;
     benchq) timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/benchq.json" 2> "$out/benchq.err" ;;
@@ -46,6 +48,20 @@ for step in "$@"; do
       rm -rf "$out/pmc_${op}_$layer" ;;
     ab) REPS=${REPS:-3} bash tools/ab_bench.sh ${val//,/ } >> "$out/ab.txt" 2>&1 ;;
     ops) bash tools/ab_ops.sh ${val//,/ } >> "$out/ops.txt" 2>&1 ;;
+    envops)
+      for v in 0 default; do
+        echo "== $val=$v" >> "$out/envops.txt"
+        for op in ${OPS:-fwd dgrad}; do for l in ${LAYERS:-b4c3 b3c3 b2c3 b1c3 b4c1 b3c1}; do
+          if [ $v = default ]; then timeout -k 5 60 python3 tools/op_bench.py $op $l >> "$out/envops.txt" 2>&1
+          else env $val=0 timeout -k 5 60 python3 tools/op_bench.py $op $l >> "$out/envops.txt" 2>&1; fi
+        done; done
+      done ;;
+    envab)
+      for r in $(seq ${REPS:-3}); do for v in 0 default; do
+        if [ $v = default ]; then timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/envab.tmp" 2>&1
+        else env $val=0 timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/envab.tmp" 2>&1; fi
+        echo "$val=$v $(tail -1 "$out/envab.tmp" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" >> "$out/envab.txt"
+      done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
