@@ -33,6 +33,20 @@
 #include "conv.h"
 #include <cstdlib>
 
+#ifdef DB_DBG_TIMING
+// A/B only: per-wave segment stamps (s_memtime) of stream items 16-23, blocks 0-7, 10 stamps
+// per item: load-segment start, after the epilogue work, after the DMA issue, after the fragment
+// reads (lgkmcnt 0), after group 1's vmcnt wait, after barrier A, after the MFMAs, after group
+// 0's vmcnt wait, after barrier B
+__device__ unsigned long long g_db_dbg[8 * 8 * 8 * 10];
+#define DB_TS(it, k)                                                                             \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 8 && (it) >= 16 && (it) < 24)                     \
+    g_db_dbg[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + ((it) - 16)) * 10 + (k)] =             \
+        __builtin_amdgcn_s_memtime()
+#else
+#define DB_TS(it, k)
+#endif
+
 namespace {
 
 constexpr int DB_THREADS = 512;
@@ -306,7 +320,9 @@ __global__ __launch_bounds__(DB_THREADS, 1) void conv_nt_db_kernel(ConvArgs a) {
       const char* buf = smem + (g % DB_NBUF) * DB_BUF;
       // ---- load segment: the previous tile's epilogue work first (its temporaries are dead
       // before the fragments go live), then the DMA of item g + 2, then this item's fragments
+      DB_TS(g, 0);
       int s = 0;
+#ifndef DB_NOSTORE
       if (has_prev) {
         if (stats && kb == 0) {
           stats1(QC);
@@ -323,19 +339,28 @@ __global__ __launch_bounds__(DB_THREADS, 1) void conv_nt_db_kernel(ConvArgs a) {
         DB_STQ(0) DB_STQ(1) DB_STQ(2) DB_STQ(3) DB_STQ(4) DB_STQ(5) DB_STQ(6) DB_STQ(7)
 #undef DB_STQ
       }
+#endif
+      DB_TS(g, 1);
       const int p = issue_next();   // item g + 2
+      DB_TS(g, 2);
       read_frags(buf);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      DB_TS(g, 3);
       const bool more = g + 1 < issued;   // item g + 1 exists (its DMA is out)
       // item g + 1's DMA went out at the end of the previous load segment's VMEM work: after it
       // come this segment's stores and DMA
       const int nwait = s + p;
       if (grp == 1 && more) vm_wait(nwait);
+      DB_TS(g, 4);
       db_barrier();
+      DB_TS(g, 5);
       // ---- MFMA segment ----
       mfma_all(PC);
+      DB_TS(g, 6);
       if (grp == 0 && more) vm_wait(nwait);
+      DB_TS(g, 7);
       db_barrier();
+      DB_TS(g, 8);
     }
   };
 
@@ -418,3 +443,9 @@ hipError_t launch_conv_nt_db(int dtype, const ConvArgs& a, hipStream_t s) {
   if (dtype == SEG_F16) return db_launch<f16_t>(a, s);
   return db_launch<bf16_t>(a, s);
 }
+
+#ifdef DB_DBG_TIMING
+extern "C" int seg_dbg_db_timing(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_db_dbg), sizeof(g_db_dbg)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -33,8 +33,12 @@ under that mask must equal the native counts exactly (proof that the captured de
 the loss head's own), and the oracle's own gate may differ from the native one on at most
 0.1 % of a weak image's pixels per head (the flip count, asserted separately).
 
-Tolerances: per-step losses at rtol 1e-3 with no absolute slack, all four terms, read from
-the device after each step's train_op (fp32 scalars, not the 4-decimal log line);
+Tolerances: the losses are read from the device after each step's train_op (fp32 scalars, not
+the 4-decimal log line), all four terms, with no absolute slack: step 0 (both sides from the same
+weights and inputs) at rtol 1e-3; steps 1-2 follow updated weights, whose gradients carry the
+ill-conditioned early-layer error of every fp32 implementation (test_gpu_step.py's docstring),
+so each term there is held to max(1e-3, 3 x the fp32 oracle's own relative gap on that term)
+(measured: the fp32 oracle's l2h at step 2 of the strong-bbox-tag run is 6.5e-4 off fp64);
 the parameter, momentum and EMA changes over the three steps (w3 - w0, v3, e3 - w0, all
 trainable tensors flattened, L2-relative) max(1e-2, 3 x the fp32 oracle's own gap on the same
 quantity); BN moving statistics max(1e-3, 4 x that gap).
@@ -71,6 +75,16 @@ def _capture_weak_decisions(monkeypatch, captured):
         captured.append((d1, L.counts()))
         return L
     monkeypatch.setattr(deh, "define_losses", wrapped)
+
+
+def _check_losses(logged, ref_losses, l32):
+    """Device loss terms vs the fp64 oracle chain: step 0 at rtol 1e-3; later steps at
+    max(1e-3, 3 x the fp32 oracle chain's own relative gap), per term (module docstring)."""
+    for k, (got, ref, r32) in enumerate(zip(logged, ref_losses, l32)):
+        got, ref, r32 = np.array(got), np.array(ref), np.array(r32)
+        scale = np.maximum(np.abs(ref), 1e-30)
+        tol = 1e-3 if k == 0 else np.maximum(1e-3, 3 * np.abs(r32 - ref) / scale)
+        assert np.all(np.abs(got - ref) <= tol * scale), (k, got, ref, r32)
 
 
 def _capture_device_losses(monkeypatch, out):
@@ -177,9 +191,7 @@ def test_train_main_matches_oracle_trajectory(cuda, tmp_path, capsys, monkeypatc
     ref_losses, ref_p, ref_m, ref_e, flips = chain(torch.float64)
     l32, p32, m32, e32, _ = chain(torch.float32)
     # every term at 1e-3: with weak images both chains use the native weak-weight mask
-    for k, (got, ref) in enumerate(zip(logged, ref_losses)):
-        got, ref = np.array(got), np.array(ref)
-        assert np.all(np.abs(got - ref) <= 1e-3 * np.abs(ref)), (k, got, ref, l32[k])
+    _check_losses(logged, ref_losses, l32)
     # the gate itself, counted separately: the oracle's own argmax moves at most 0.1 % of a
     # weak image's pixels in or out of a head's weights (measured: <= 1 px at step 0, where
     # both start from the same weights; <= 4 of 8192 px at steps 1-2, where the trajectories
@@ -329,9 +341,7 @@ def test_train_main_real_data_matches_oracle(cuda, tmp_path, capsys, monkeypatch
 
     ref_losses, ref_p, ref_m, ref_e, flips = chain(torch.float64)
     l32, p32, m32, e32, _ = chain(torch.float32)
-    for k, (got, ref) in enumerate(zip(logged, ref_losses)):
-        got, ref = np.array(got), np.array(ref)
-        assert np.all(np.abs(got - ref) <= 1e-3 * np.abs(ref)), (k, got, ref, l32[k])
+    _check_losses(logged, ref_losses, l32)
     assert all(int(f.max()) <= max(2, H * W // 1000) for f in flips), flips
     nat_p, nat_m, nat_e = ctx.named("params"), ctx.named("momentum"), ctx.named("ema")
     keys = list(ref_m)

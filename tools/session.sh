@@ -49,6 +49,7 @@ for step in "$@"; do
     ab) REPS=${REPS:-3} bash tools/ab_bench.sh ${val//,/ } >> "$out/ab.txt" 2>&1 ;;
     ops) bash tools/ab_ops.sh ${val//,/ } >> "$out/ops.txt" 2>&1 ;;
     envops)
+      [ "$val" = envops ] && { echo "envops needs =VAR"; exit 2; }
       for v in 0 default; do
         echo "== $val=$v" >> "$out/envops.txt"
         for op in ${OPS:-fwd dgrad}; do for l in ${LAYERS:-b4c3 b3c3 b2c3 b1c3 b4c1 b3c1}; do
@@ -57,6 +58,7 @@ for step in "$@"; do
         done; done
       done ;;
     envab)
+      [ "$val" = envab ] && { echo "envab needs =VAR"; exit 2; }
       for r in $(seq ${REPS:-3}); do for v in 0 default; do
         if [ $v = default ]; then timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/envab.tmp" 2>&1
         else env $val=0 timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/envab.tmp" 2>&1; fi
