@@ -416,14 +416,15 @@ hipError_t db_launch(const ConvArgs& a, hipStream_t s) {
 
 }  // namespace
 
-// SEG_NT_DB=0 turns the path off (A/B against the 256 x 256 ping-pong kernel); SEG_NT_DB_MAXK
-// sets the longest reduction it takes (default 512)
+// Off by default (measured slower than the 256 x 256 ping-pong kernel on every short-K layer,
+// DESIGN.md §5d); SEG_NT_DB=1 turns it on for A/B, SEG_NT_DB_MAXK sets the longest reduction
+// it takes (default 512)
 static int db_max_k() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SEG_NT_DB");
     const char* k = getenv("SEG_NT_DB_MAXK");
-    v = (e && e[0] == '0') ? 0 : (k ? atoi(k) : 512);
+    v = !(e && e[0] == '1') ? 0 : (k ? atoi(k) : 512);
     if (v > DB_MAX_K) v = DB_MAX_K;
   }
   return v;

@@ -16,8 +16,8 @@
 #   pmc=OP:LAYER          PMC counter passes of one single-op bench (OP fwd|dgrad|wgrad)
 #   ab=V1,V2,...          interleaved whole-step A/B: the in-tree library vs ab/Vi/libseg_hip.so
 #   ops=V1,V2,...         single-op A/B on the same variants (OPS / LAYERS env override)
-#   envops=VAR            single-op A/B: VAR=0 vs unset (OPS / LAYERS env override)
-#   envab=VAR             interleaved whole-step A/B (benchq): VAR=0 vs unset, REPS rounds
+#   envops=VAR[:A:B]      single-op A/B: VAR=A (default 0) vs VAR=B (default unset; OPS / LAYERS)
+#   envab=VAR[:A:B]       interleaved whole-step A/B (benchq) of the same two arms, REPS rounds
 set -e
 tag=$1; shift
 out=gpurun_out/$tag
@@ -50,19 +50,21 @@ for step in "$@"; do
     ops) bash tools/ab_ops.sh ${val//,/ } >> "$out/ops.txt" 2>&1 ;;
     envops)
       [ "$val" = envops ] && { echo "envops needs =VAR"; exit 2; }
-      for v in 0 default; do
-        echo "== $val=$v" >> "$out/envops.txt"
+      IFS=: read -r var va vb <<< "$val"
+      for v in "${va:-0}" "${vb:-default}"; do
+        echo "== $var=$v" >> "$out/envops.txt"
         for op in ${OPS:-fwd dgrad}; do for l in ${LAYERS:-b4c3 b3c3 b2c3 b1c3 b4c1 b3c1}; do
-          if [ $v = default ]; then timeout -k 5 60 python3 tools/op_bench.py $op $l >> "$out/envops.txt" 2>&1
-          else env $val=0 timeout -k 5 60 python3 tools/op_bench.py $op $l >> "$out/envops.txt" 2>&1; fi
+          if [ "$v" = default ]; then timeout -k 5 60 python3 tools/op_bench.py $op $l >> "$out/envops.txt" 2>&1
+          else env $var=$v timeout -k 5 60 python3 tools/op_bench.py $op $l >> "$out/envops.txt" 2>&1; fi
         done; done
       done ;;
     envab)
       [ "$val" = envab ] && { echo "envab needs =VAR"; exit 2; }
-      for r in $(seq ${REPS:-3}); do for v in 0 default; do
-        if [ $v = default ]; then timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/envab.tmp" 2>&1
-        else env $val=0 timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/envab.tmp" 2>&1; fi
-        echo "$val=$v $(tail -1 "$out/envab.tmp" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" >> "$out/envab.txt"
+      IFS=: read -r var va vb <<< "$val"
+      for r in $(seq ${REPS:-3}); do for v in "${va:-0}" "${vb:-default}"; do
+        if [ "$v" = default ]; then timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/envab.tmp" 2>&1
+        else env $var=$v timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > "$out/envab.tmp" 2>&1; fi
+        echo "$var=$v $(tail -1 "$out/envab.tmp" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" >> "$out/envab.txt"
       done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
