@@ -113,8 +113,12 @@ int seg_set_nesterov(seg_ctx* ctx, int on);
  * returns with the stream joined to every weight gradient except the stem's, which is still
  * running on the weight-gradient stream; seg_apply_update updates every other parameter beside
  * it and joins before the stem's weights. Every other call that takes a stream joins first.
- * No reference counterpart (scheduling only; results are unchanged). Off by default. */
+ * No reference counterpart (scheduling only; results are unchanged). Off by default.
+ * With on, seg_backward also defers every other layer's split-K weight-gradient reduce: they
+ * run as one batched launch at the start of seg_apply_update (bitwise the same gradients);
+ * seg_flush_grads runs them on `stream` for a caller that reads the gradient buffer first. */
 int seg_set_defer_stem(seg_ctx* ctx, int on);
+int seg_flush_grads(seg_ctx* ctx, void* stream);
 /* pre-masked identity-unit gradients (on by default): when an identity unit follows another,
  * its conv1 data gradient stores the previous unit's output gradient already ReLU-masked, and
  * that unit's c3 BN backward skips the mask bits and the separate masked-gradient store.

@@ -55,6 +55,10 @@ struct WgradArgs {
 // host launchers (conv.hip); return hipError_t
 hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s);
+// every deferred split-K reduce of a step in one launch (blockIdx.y = job); per element the
+// same slab-order sum as launch_splitk_reduce (bitwise-identical gradients)
+struct ReduceJob { const float* part; float* out; long n, stride; int splits; };
+hipError_t launch_splitk_reduce_batched(const ReduceJob* jobs, int njobs, hipStream_t s);
 hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride, long n,
                                 float* out, int accumulate, hipStream_t s);
 // all layers' flips in one launch: table of FlipJob (device), prefix = the job's first tile;

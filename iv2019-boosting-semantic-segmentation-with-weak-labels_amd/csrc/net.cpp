@@ -211,6 +211,19 @@ struct seg_ctx {
   // workspace
   float* slab = nullptr;
   size_t slab_floats = 0;
+  // deferred split-K reduces (round 5): with seg_set_defer_stem (one process: nothing reads the
+  // gradients between backward and update) every weight gradient but the stem's writes its own
+  // slab region and ALL their reduces run as one launch at the start of seg_apply_update (or
+  // seg_flush_grads), instead of one reduce per layer on the weight-gradient stream beside the
+  // data-gradient chain
+  float* slab_all = nullptr;
+  std::vector<long> slab_off;      // per conv: its region in slab_all (-1 = none)
+  std::vector<long> slab_cap;      // per conv: floats in that region
+  ReduceJob* red_jobs = nullptr;   // device table, one job per deferred layer (jobs built per step)
+  std::vector<ReduceJob> red_host, red_dev;   // this step's jobs / the device table's copy
+  bool defer_red_on = true;        // SEG_DEFER_REDUCE=0 at creation: off (A/B)
+  bool defer_red = false;          // this step's non-stem reduces are deferred
+  bool red_pending = false;        // ... and have not run yet
   float* stat_scratch = nullptr;
   size_t stat_scratch_floats = 0;
   Prof prof;
@@ -813,6 +826,7 @@ int bucket_progress(seg_ctx* c, hipStream_t ws, bool final) {
 }
 
 int conv_wgrad_impl(Step& S, int li, const Act& x);
+int flush_reduces(seg_ctx* c, hipStream_t s);
 int conv_wgrad(Step& S, int li, const Act& x) {
   seg_ctx* c = S.c;
   Step W = S;
@@ -844,11 +858,13 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   // runs beside it, so it takes the whole chip (tools/timeline.py: the compute stream idled
   // ~0.75 ms waiting for it)
   a.splits = wgrad_splits(a, S.dt, c->side_active && li != c->stem);
-  {  // the slab was sized at creation for these shapes; never exceed it
-    const long per = (long)a.Co * a.KH * a.KW * a.C;
+  const long per = (long)a.Co * a.KH * a.KW * a.C;
+  // deferred reduce: this layer's own slab region, the reduce joins the step's batched one
+  const bool defer = c->defer_red && li != c->stem && !s2d && c->slab_off[li] >= 0 &&
+                     (long)a.splits * per <= c->slab_cap[li];
+  if (!defer)  // the shared slab was sized at creation for these shapes; never exceed it
     a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / per));
-  }
-  a.out = c->slab;
+  a.out = defer ? c->slab_all + c->slab_off[li] : c->slab;
   long P = (long)L.N * L.Ho * L.Wo;
   int slot;
   // dy + x (16-bit) + the fp32 weight gradient; split-K slab traffic is overhead, not algorithmic
@@ -865,6 +881,11 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   const long n = (long)L.co * L.k * L.k * L.ci;
   // slab rows are co_pad wide only in the Co dimension: rows 0..co-1 are the real ones
   // split z of the slab starts at z*co_pad*ncol; rows >= co are padding and never reduced
+  if (defer) {
+    c->red_host.push_back({a.out, c->grads + L.w_off, n, (long)L.co_pad * L.k * L.k * L.ci, a.splits});
+    c->red_pending = true;
+    return 0;
+  }
   HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, (long)L.co_pad * L.k * L.k * L.ci, n,
                                   c->grads + L.w_off, 0, S.s));
   return 0;
@@ -1228,6 +1249,25 @@ int build(seg_ctx* c) {
   }
   c->slab_floats = slab;
   if (int r = dalloc(c, &c->slab, slab)) return r;
+  {  // per-layer regions for the deferred reduces (side-stream split counts; not the stem's)
+    size_t tot = 0;
+    c->slab_off.assign(c->convs.size(), -1);
+    c->slab_cap.assign(c->convs.size(), 0);
+    for (size_t li = 0; li < c->convs.size(); ++li) {
+      if ((int)li == c->stem) continue;
+      const ConvL& L = c->convs[li];
+      const WgradArgs a = wgrad_problem(L, false);
+      const size_t per = (size_t)a.Co * a.KH * a.KW * a.C;
+      c->slab_off[li] = (long)tot;
+      c->slab_cap[li] = (long)(per * wgrad_splits(a, c->dt, true));
+      tot += (size_t)c->slab_cap[li];
+      tot = (tot + 63) / 64 * 64;   // 256-B aligned regions
+    }
+    const char* e = getenv("SEG_DEFER_REDUCE");
+    c->defer_red_on = !(e && e[0] == '0');
+    if (int r = dalloc(c, &c->slab_all, std::max<size_t>(c->defer_red_on ? tot : 0, 64))) return r;
+    if (int r = dalloc(c, &c->red_jobs, c->convs.size())) return r;
+  }
   if (int r = dalloc(c, &c->stat_scratch, std::max<size_t>(c->stat_scratch_floats, 16))) return r;
   return 0;
 }
@@ -1441,8 +1481,16 @@ int backward(Step& S) {
   std::fill(c->wg_done.begin(), c->wg_done.end(), 0);
   c->bk_next = 0;
   // a profiled backward runs on one stream so the HIP-event kernel timings are kernel-alone
+  // a previous backward whose deferred reduces no update consumed: run them before the side
+  // stream (ordered after this point by ev_join) rewrites the slabs
+  if (int r = flush_reduces(c, S.s)) return r;
   c->side_active = c->side_on && !c->prof.on;
   c->prestem_rec = false;
+  // one process with a deferred stem: nothing reads the gradients before seg_apply_update, so
+  // every other layer's split-K reduce joins one batched launch there (not with loss scaling:
+  // seg_set_defer_stem is never set for fp16, and the overflow check reads the gradients)
+  c->defer_red = c->side_active && c->defer_stem && !c->skip_flag && c->slab_all && c->defer_red_on;
+  c->red_host.clear();
   if (c->side_active) {   // the side stream must not run ahead of the previous use of its buffers
     HIPCALL(c, hipEventRecord(c->ev_join, S.s));
     HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
@@ -1560,6 +1608,23 @@ int refresh_stem_pad(seg_ctx* c, hipStream_t s) {
 // on stream s reads or rewrites the step's buffers. The pending state is kept until the
 // gradient is consumed (seg_apply_update) or superseded (seg_backward): a join on another
 // stream must not let a later seg_apply_update skip its own join
+// the deferred split-K reduces of the step, on stream s (whose work already follows every
+// non-stem weight gradient: seg_backward's join on ev_prestem / ev_join)
+int flush_reduces(seg_ctx* c, hipStream_t s) {
+  if (!c->red_pending) return 0;
+  const int nj = (int)c->red_host.size();
+  // the table is the same every step (layers, regions, split counts): copied when it changes
+  if (c->red_dev.size() != c->red_host.size() ||
+      memcmp(c->red_dev.data(), c->red_host.data(), nj * sizeof(ReduceJob))) {
+    HIPCALL(c, hipStreamSynchronize(s));   // no launch of the previous table is still reading it
+    HIPCALL(c, hipMemcpy(c->red_jobs, c->red_host.data(), nj * sizeof(ReduceJob), hipMemcpyHostToDevice));
+    c->red_dev = c->red_host;
+  }
+  HIPCALL(c, launch_splitk_reduce_batched(c->red_jobs, nj, s));
+  c->red_pending = false;
+  return 0;
+}
+
 int join_stem(seg_ctx* c, hipStream_t s, bool consume = false) {
   if (!c->stem_pending) return 0;
   HIPCALL(c, hipStreamWaitEvent(s, c->ev_join, 0));
@@ -1803,6 +1868,7 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
                      st_hi <= c->n_decay;
   if (!split)
     if (int r = join_stem(c, s, true)) return r;
+  if (int r = flush_reduces(c, s)) return r;
   if (c->skip_flag) {   // loss-scaled (fp16) step: unscale, and skip it if anything overflowed
     HIPCALL(c, hipMemsetAsync(c->skip_flag, 0, sizeof(int), s));
     HIPCALL(c, launch_nonfinite(c->grads, c->n_train, c->skip_flag, s));
@@ -1866,6 +1932,11 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
     HIPCALL(c, launch_sum_partials(c->reg_part, nparts, c->reg_out, s));
   }
   return refresh_stem_pad(c, s);
+}
+
+int seg_flush_grads(seg_ctx* c, void* stream) {
+  NEED_BOUND(c);
+  return flush_reduces(c, (hipStream_t)stream);
 }
 
 int seg_set_defer_stem(seg_ctx* c, int on) {

@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = [
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
     "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict", "seg_full_predictions",
-    "seg_set_nesterov", "seg_set_defer_stem", "seg_set_premask", "seg_counter",
+    "seg_set_nesterov", "seg_set_defer_stem", "seg_flush_grads", "seg_set_premask", "seg_counter",
     "seg_crc32c", "seg_prepare_images", "seg_prepare_labels", "seg_prepare_images_crop",
 ]
 
@@ -120,6 +120,7 @@ def _load():
         "seg_full_predictions": (ip, [vp, vp, vp, vp, vp, vp]),
         "seg_set_nesterov": (ip, [vp, ip]),
         "seg_set_defer_stem": (ip, [vp, ip]),
+        "seg_flush_grads": (ip, [vp, vp]),
         "seg_set_premask": (ip, [vp, ip]),
         "seg_counter": (ip, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     }
@@ -230,6 +231,8 @@ class SegContext:
         """Host copies of named tensors of params/grads/momentum/ema."""
         buf = {"params": self.params, "grads": self.grads, "momentum": self.momentum,
                "ema": self.ema}[buffer]
+        if buffer == "grads":   # deferred split-K reduces (seg_set_defer_stem) run first
+            self.flush_grads()
         out = {}
         for p in self.param_info:
             if p.kind in ("moving_mean", "moving_variance"):
@@ -239,6 +242,11 @@ class SegContext:
             if src is not None:
                 out[p.name] = src[p.offset:p.offset + p.numel].detach().cpu().numpy()
         return out
+
+    def flush_grads(self, stream=None):
+        """Run the step's deferred split-K reduces (seg_set_defer_stem) so the gradient buffer
+        is complete; a no-op otherwise."""
+        check(LIB.seg_flush_grads(self.h, _stream(stream)), self.h)
 
     # ---- step -----------------------------------------------------------------------
     def forward(self, images, stream=None):

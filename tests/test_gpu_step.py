@@ -211,8 +211,11 @@ def test_bf16_step_is_deterministic(cuda):
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 def test_defer_stem_update_matches(cuda, dtype):
     """seg_set_defer_stem (the update of every parameter but the stem's beside the stem's weight
-    gradient, then the stem's): three steps with EMA give bitwise the same parameters, momentum
-    and EMA shadows as the joined update; the regulariser value (a sum in another order) 1e-6."""
+    gradient, then the stem's; every other layer's split-K reduce deferred to one batched launch
+    at the update): three steps with EMA give bitwise the same parameters, momentum and EMA
+    shadows as the joined update, and the last step's gradients (read between backward and
+    update through seg_flush_grads) are bitwise the per-layer reduces'; the regulariser value (a
+    sum in another order) 1e-6."""
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp")
@@ -232,13 +235,17 @@ def test_defer_stem_update_matches(cuda, dtype):
             ctx.forward(img)
             ctx.loss(px, bb, None)
             ctx.backward()
+            if step == 2:
+                grads = ctx.named("grads")
             ctx.apply_update(0.01, 0.9, min(0.9, (1.0 + step) / (10.0 + step)))
             torch.cuda.synchronize()
             regs.append(float(ctx.outputs()[1].cpu().numpy()[0]))
         out.append((ctx.named("params"), ctx.momentum.cpu().numpy().copy(),
-                    ctx.ema.cpu().numpy().copy(), regs))
+                    ctx.ema.cpu().numpy().copy(), regs, grads))
         ctx.close()
-    (p0, m0, e0, r0), (p1, m1, e1, r1) = out
+    (p0, m0, e0, r0, g0), (p1, m1, e1, r1, g1) = out
+    for k in g0:
+        assert np.array_equal(g0[k], g1[k]), k
     for k in p0:
         assert np.array_equal(p0[k], p1[k]), k
     assert np.array_equal(m0, m1) and np.array_equal(e0, e1)
