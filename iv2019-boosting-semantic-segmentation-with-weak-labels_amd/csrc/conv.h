@@ -39,6 +39,17 @@ struct ConvArgs {
   // outputs whose bit is 0 are stored as zero (conv_nt_omask_ok launches only)
   const uint8_t* omask;
   int ldm;
+  // optional BN-backward reduce of the layer whose output gradient this data gradient is
+  // (ping-pong one-tile launches, no residual): per 256-row tile and channel the partial
+  // (sum dyhat, sum dyhat * xhat) with dyhat = out * ReLU bit, xhat = (bq_y - mean) * invstd,
+  // into bq_part [tiles][Co][2] (the separate bn_bwd_reduce8 pass's input, folded)
+  const void* bq_y;
+  int bq_ldy;
+  const uint8_t* bq_mask;
+  int bq_ldm;
+  const float* bq_mean;
+  const float* bq_invstd;
+  float* bq_part;
 };
 
 struct WgradArgs {
@@ -91,6 +102,8 @@ hipError_t launch_conv_nt_db(int dtype, const ConvArgs& a, hipStream_t s);
 // launches that apply ConvArgs::omask: 16-bit dense 1x1 ping-pong with a residual (one tile per
 // workgroup), i.e. the identity units' conv1 data gradient
 bool conv_nt_omask_ok(int dtype, const ConvArgs& a);
+// launches that can fold the BN-backward reduce (ConvArgs::bq_*) into the epilogue
+bool conv_nt_bq_ok(int dtype, const ConvArgs& a);
 // ping-pong 256x256 weight gradient (conv_pp.hip), used when the v2 tile choice is 256 x 256
 bool conv_wgrad_pp_ok(const WgradArgs& a);
 hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s);

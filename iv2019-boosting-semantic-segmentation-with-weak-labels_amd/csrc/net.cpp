@@ -61,6 +61,10 @@ struct ConvL {
   float* stats_part = nullptr;    // [mtiles][co][2]
   float* bwd_part = nullptr;      // [rb][co][2] (group norm: [N][rb][co][2], rb per image)
   int rb = 1;
+  // the BN-backward reduce folded into the producing data gradient's epilogue (round 5,
+  // ConvArgs::bq_*): per 256-row tile partials [ceil(M/256)][co][2]; nullptr = not foldable
+  float* bq_part = nullptr;
+  bool bq_ready = false;          // this step's partials were written by the data gradient
   // group norm: groups, per-image states (host copies of the device array st_dev) and the
   // forward chunk partials
   int groups = 0;
@@ -222,6 +226,7 @@ struct seg_ctx {
   ReduceJob* red_jobs = nullptr;   // device table, one job per deferred layer (jobs built per step)
   std::vector<ReduceJob> red_host, red_dev;   // this step's jobs / the device table's copy
   bool defer_red_on = true;        // SEG_DEFER_REDUCE=0 at creation: off (A/B)
+  bool bq_on = false;              // SEG_BN_FOLD=1 at creation: BN-backward reduce folded (A/B)
   bool defer_red = false;          // this step's non-stem reduces are deferred
   bool red_pending = false;        // ... and have not run yet
   float* stat_scratch = nullptr;
@@ -429,6 +434,8 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
     if (int r = dalloc(c, &L.st_dev, (size_t)N)) return r;
     HIPCALL(c, hipMemcpy(L.st_dev, L.st_img.data(), N * sizeof(BnState), hipMemcpyHostToDevice));
   } else {
+    if (L.co > 128 && seg_half(c->dt))   // the ping-pong data gradients' width (Co > 128)
+      if (int r = dalloc(c, &L.bq_part, (size_t)ceil_div(M, 256) * L.co * 2)) return r;
     L.rb = bn_bwd_rowblocks(M, L.co);
     if (int r = dalloc(c, &L.bwd_part, (size_t)L.rb * L.co * 2)) return r;
   }
@@ -635,13 +642,19 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   const double me = a.M * (double)a.C * 1e-9;
   const double gb_in = me * (zsz + (a.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
   int slot;
-  if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
-  HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
-  if (int r = prof_end(c, S.s, slot)) return r;
+  // folded (conv_dgrad with bn_li): the data gradient's epilogue already wrote the partials
+  const bool folded = L.bq_ready;
+  L.bq_ready = false;
+  if (!folded) {
+    if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
+    HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
+    if (int r = prof_end(c, S.s, slot)) return r;
+  }
   const bool tb = c->cfg.train_bn != 0;
   // a backward after a moving-statistics forward (TRAIN without
   // batch_norm_accumulate_statistics) differentiates through constant statistics
-  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
+  HIPCALL(c, launch_bn_bwd_finalize(folded ? L.bq_part : L.bwd_part,
+                                    folded ? ceil_div(a.M, 256) : L.rb, a.M, L.co, L.st,
                                     tb ? c->grads + L.g_off : nullptr,
                                     tb ? c->grads + L.b_off : nullptr, S.s, c->bn_infer));
   if (c->sync_fn && !c->bn_infer) {
@@ -751,12 +764,23 @@ int gn_backward(Step& S, int li, const Act& dz0, int dz_f32, const Act* z0, cons
 ConvArgs dgrad_args(seg_ctx* c, int li, const Act& dx, const Act* r1, const Act* r2);
 
 // dx = dgrad(dy) [+ r1] [+ r2]
+// bn_li / bn_z: the BN layer whose output gradient dx is, and its output activation (the ReLU
+// bits): with seg_ctx::bq_on the BN-backward reduce is folded into this data gradient's
+// epilogue where the one-tile ping-pong launch can take it (then bn_backward skips its reduce)
 int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr,
-               const uint8_t* omask = nullptr) {
+               const uint8_t* omask = nullptr, int bn_li = -1, const Act* bn_z = nullptr) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
   ConvArgs a = dgrad_args(c, li, dx, r1, r2);
   if (omask) { a.omask = omask; a.ldm = a.Co / 8; }
+  if (bn_li >= 0 && c->bq_on && !c->gn && bn_z && bn_z->mask) {
+    ConvL& B = c->convs[bn_li];
+    if (B.bq_part && bn_z->C == B.co && B.co == a.Co && B.y.M() == dx.M() && conv_nt_bq_ok(S.dt, a)) {
+      a.bq_y = B.y.p; a.bq_ldy = B.y.ld; a.bq_mask = bn_z->mask; a.bq_ldm = (B.co + 7) / 8;
+      a.bq_mean = B.st.mean; a.bq_invstd = B.st.invstd; a.bq_part = B.bq_part;
+      B.bq_ready = true;
+    }
+  }
   long M = (long)L.N * L.H * L.W;
   int slot;
   // dy + w + dx (+ each residual read once)
@@ -765,7 +789,8 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
                       (double)M * L.ci * (1.0 + nres)) * c->esz * 1e-9;
   if (int r = prof_begin(c, S.s, 1, li, 2.0 * M * L.ci * L.k * L.k * L.co * 1e-9 / L.stride / L.stride,
                          &slot, gbx)) return r;
-  HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
+  if (a.bq_part) HIPCALL(c, launch_conv_nt_pp(S.dt, a, S.s));
+  else HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   return prof_end(c, S.s, slot);
 }
 
@@ -1265,6 +1290,8 @@ int build(seg_ctx* c) {
     }
     const char* e = getenv("SEG_DEFER_REDUCE");
     c->defer_red_on = !(e && e[0] == '0');
+    const char* f = getenv("SEG_BN_FOLD");
+    c->bq_on = f && f[0] == '1';
     if (int r = dalloc(c, &c->slab_all, std::max<size_t>(c->defer_red_on ? tot : 0, 64))) return r;
     if (int r = dalloc(c, &c->red_jobs, c->convs.size())) return r;
   }
@@ -1325,10 +1352,10 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred =
       if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
   }
   if (int r = conv_wgrad(S, u.c3, u.z2)) return r;
-  if (int r = conv_dgrad(S, u.c3, u.dz2)) return r;
+  if (int r = conv_dgrad(S, u.c3, u.dz2, nullptr, nullptr, nullptr, u.c2, &u.z2)) return r;
   if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr)) return r;
   if (int r = conv_wgrad(S, u.c2, u.z1)) return r;
-  if (int r = conv_dgrad(S, u.c2, u.dz1)) return r;
+  if (int r = conv_dgrad(S, u.c2, u.dz1, nullptr, nullptr, nullptr, u.c1, &u.z1)) return r;
   if (int r = bn_backward(S, u.c1, u.dz1, 0, &u.z1, nullptr)) return r;
   if (int r = conv_wgrad(S, u.c1, u.in)) return r;
   switch (u.kind) {

@@ -299,6 +299,43 @@ def test_premask_matches(cuda, dtype, depth):
     assert np.array_equal(m0, m1)
 
 
+def test_bn_fold_matches(cuda, monkeypatch):
+    """SEG_BN_FOLD=1 (round 5): the BN-backward reduce of the units' conv1 /
+    conv2 BN layers folded into the epilogue of the data gradient that produces their output
+    gradient (one-tile ping-pong launches, Co > 128: blocks 3-4). Only the order of the fp32
+    partial sums differs from the separate reduce pass, so one bf16 step agrees with the unfolded
+    step to 1e-2 on every gradient (bf16 rounding of the data gradients downstream) and to 1e-4
+    on the gamma / beta gradients of block4's last unit (the first folded layers, same inputs)."""
+    from input_pipelines.synthetic import batch
+    from seg_hip import SegContext
+    cfg = SegConfig(height=64, width=128, nb_pp=2, pyramid="aspp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=13).items()}
+    data = batch(24, cfg.nb_pp, 0, 0, cfg.height, cfg.width)
+    img = torch.as_tensor(data["images"]).to(cuda)
+    px = torch.as_tensor(data["px"]).to(cuda)
+    out = []
+    for fold in ("0", "1"):
+        monkeypatch.setenv("SEG_BN_FOLD", fold)   # read at context creation
+        ctx = SegContext(pyramid=cfg.pyramid, height=cfg.height, width=cfg.width, nb_pp=2,
+                         dtype="bf16")
+        ctx.load_params(params)
+        ctx.forward(img)
+        ctx.loss(px, None, None)
+        ctx.backward()
+        torch.cuda.synchronize()
+        out.append((ctx.outputs()[0].cpu().numpy().copy(), ctx.named("grads")))
+        ctx.close()
+    (l0, g0), (l1, g1) = out
+    assert np.array_equal(l0, l1)   # the forward and the loss head are untouched
+    bad = [(k, _rel(g1[k], g0[k])) for k in g0 if _rel(g1[k], g0[k]) > 1e-2]
+    assert not bad, sorted(bad, key=lambda t: -t[1])[:10]
+    last = "feature_extractor/base/resnet_v1_50/block4/unit_3/bottleneck_v1/conv2/BatchNorm"
+    for t in ("gamma", "beta"):
+        assert _rel(g1[f"{last}/{t}"], g0[f"{last}/{t}"]) < 1e-4, t
+    # the folded path really ran: the reduced-once gradients are not bitwise the unfolded ones
+    assert any(not np.array_equal(g1[k], g0[k]) for k in g0 if "block4" in k)
+
+
 def test_defer_stem_join_on_other_stream(cuda):
     """with defer on, a join-taking call on another stream (seg_predict on B) between
     seg_backward and seg_apply_update (both on A) must not consume the pending stem join: the
