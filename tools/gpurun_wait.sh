@@ -7,7 +7,7 @@ log=$1; to=$2; shift 2
 for i in $(seq 40); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@" > "$log" 2>&1
   rc=$?
-  if [ $rc -eq 3 ] || grep -q "slot(s) on this pod are busy" "$log"; then
+  if [ $rc -eq 3 ] || grep -q "slot(s) on this pod are busy\|status=transient" "$log"; then
     sleep 90
     continue
   fi
