@@ -126,8 +126,9 @@ int seg_flush_grads(seg_ctx* ctx, void* stream);
  * No reference counterpart. */
 int seg_set_premask(seg_ctx* ctx, int on);
 /* runtime counters since seg_create (diagnostics; no reference counterpart):
- * "premask_launches" = conv1 data gradients stored pre-masked (seg_set_premask).
- * -ENOENT for an unknown name. */
+ * "premask_launches" = conv1 data gradients stored pre-masked (seg_set_premask);
+ * "bn_fold_launches" = data gradients whose epilogue also ran the consumer BN's backward
+ * reduce (SEG_BN_FOLD=1 at seg_create). -ENOENT for an unknown name. */
 int seg_counter(seg_ctx* ctx, const char* name, int64_t* value);
 
 /* outputs ------------------------------------------------------------------------------

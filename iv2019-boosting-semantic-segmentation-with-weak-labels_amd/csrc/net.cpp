@@ -207,6 +207,7 @@ struct seg_ctx {
   bool defer_stem = false;
   bool premask = true;             // seg_set_premask: pre-masked identity-unit gradients (unit_backward)
   int64_t premask_launches = 0;    // conv1 data gradients stored pre-masked (seg_counter)
+  int64_t bq_launches = 0;         // data gradients with the BN-backward reduce folded (seg_counter)
   bool prestem_rec = false;
   bool stem_pending = false;
   float* dzscale = nullptr;       // [ldl]
@@ -779,6 +780,7 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
       a.bq_y = B.y.p; a.bq_ldy = B.y.ld; a.bq_mask = bn_z->mask; a.bq_ldm = (B.co + 7) / 8;
       a.bq_mean = B.st.mean; a.bq_invstd = B.st.invstd; a.bq_part = B.bq_part;
       B.bq_ready = true;
+      ++c->bq_launches;
     }
   }
   long M = (long)L.N * L.H * L.W;
@@ -1982,6 +1984,7 @@ int seg_counter(seg_ctx* c, const char* name, int64_t* value) {
   if (!c || !name || !value) return set_err(c ? &c->err : nullptr, -EINVAL, "null argument");
   const std::string n(name);
   if (n == "premask_launches") *value = c->premask_launches;
+  else if (n == "bn_fold_launches") *value = c->bq_launches;
   else return set_err(&c->err, -ENOENT, "unknown counter '%s'", name);
   return 0;
 }

@@ -302,10 +302,14 @@ def test_premask_matches(cuda, dtype, depth):
 def test_bn_fold_matches(cuda, monkeypatch):
     """SEG_BN_FOLD=1 (round 5): the BN-backward reduce of the units' conv1 /
     conv2 BN layers folded into the epilogue of the data gradient that produces their output
-    gradient (one-tile ping-pong launches, Co > 128: blocks 3-4). Only the order of the fp32
-    partial sums differs from the separate reduce pass, so one bf16 step agrees with the unfolded
-    step to 1e-2 on every gradient (bf16 rounding of the data gradients downstream) and to 1e-4
-    on the gamma / beta gradients of block4's last unit (the first folded layers, same inputs)."""
+    gradient (one-tile ping-pong launches, Co > 128: blocks 3-4). Against the unfolded step on
+    the same inputs: everything the backward computes before the first folded layer (heads,
+    pyramid, decrease_fdims, block4 unit 3's conv3) bitwise equal; the first folded layer's
+    gamma / beta gradients (block4 unit 3 conv2 BN: the same dz and y, only the order of the fp32
+    partial sums differs) to 1e-5; its weight gradient (through the bf16 BN-backward output,
+    where that order can move a rounding) to 2e-2. Further down the bf16 chain a one-ulp change
+    is amplified like any bf16 rounding at random init (test_bf16_layerwise's docstring), so
+    those gradients are only required finite."""
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     cfg = SegConfig(height=64, width=128, nb_pp=2, pyramid="aspp")
@@ -324,16 +328,23 @@ def test_bn_fold_matches(cuda, monkeypatch):
         ctx.backward()
         torch.cuda.synchronize()
         out.append((ctx.outputs()[0].cpu().numpy().copy(), ctx.named("grads")))
+        # the folded launches really ran (blocks 3-4: two per unit) or really did not
+        n = ctx.counter("bn_fold_launches")
+        assert (n == 2 * (6 + 3)) if fold == "1" else (n == 0), (fold, n)
         ctx.close()
     (l0, g0), (l1, g1) = out
     assert np.array_equal(l0, l1)   # the forward and the loss head are untouched
-    bad = [(k, _rel(g1[k], g0[k])) for k in g0 if _rel(g1[k], g0[k]) > 1e-2]
-    assert not bad, sorted(bad, key=lambda t: -t[1])[:10]
-    last = "feature_extractor/base/resnet_v1_50/block4/unit_3/bottleneck_v1/conv2/BatchNorm"
+    u3 = "feature_extractor/base/resnet_v1_50/block4/unit_3/bottleneck_v1/"
+    upstream = [k for k in g0 if any(t in k for t in ("softmax_classifier", "adaptation_module",
+                                                       "pyramid_module", "extension", u3 + "conv3"))]
+    assert len(upstream) > 10
+    for k in upstream:
+        assert np.array_equal(g0[k], g1[k]), k
     for t in ("gamma", "beta"):
-        assert _rel(g1[f"{last}/{t}"], g0[f"{last}/{t}"]) < 1e-4, t
-    # the folded path really ran: the reduced-once gradients are not bitwise the unfolded ones
-    assert any(not np.array_equal(g1[k], g0[k]) for k in g0 if "block4" in k)
+        k = u3 + "conv2/BatchNorm/" + t
+        assert _rel(g1[k], g0[k]) < 1e-5, (k, _rel(g1[k], g0[k]))
+    assert _rel(g1[u3 + "conv2/weights"], g0[u3 + "conv2/weights"]) < 2e-2
+    assert all(np.all(np.isfinite(v)) for v in g1.values())
 
 
 def test_defer_stem_join_on_other_stream(cuda):
