@@ -302,14 +302,15 @@ def test_premask_matches(cuda, dtype, depth):
 def test_bn_fold_matches(cuda, monkeypatch):
     """SEG_BN_FOLD=1 (round 5): the BN-backward reduce of the units' conv1 /
     conv2 BN layers folded into the epilogue of the data gradient that produces their output
-    gradient (one-tile ping-pong launches, Co > 128: blocks 3-4). Against the unfolded step on
-    the same inputs: everything the backward computes before the first folded layer (heads,
-    pyramid, decrease_fdims, block4 unit 3's conv3) bitwise equal; the first folded layer's
-    gamma / beta gradients (block4 unit 3 conv2 BN: the same dz and y, only the order of the fp32
-    partial sums differs) to 1e-5; its weight gradient (through the bf16 BN-backward output,
-    where that order can move a rounding) to 2e-2. Further down the bf16 chain a one-ulp change
-    is amplified like any bf16 rounding at random init (test_bf16_layerwise's docstring), so
-    those gradients are only required finite."""
+    gradient (one-tile ping-pong launches, Co > 128: the bottlenecks of blocks 3-4 and the three
+    adaptation bottlenecks). Against the unfolded step on the same inputs: everything the
+    backward computes before the first folded layers (the logits convs, the adaptation units'
+    conv3) bitwise equal; the first folded layers' gamma / beta gradients (each adaptation
+    unit's conv2 BN: the same dz and y, only the order of the fp32 partial sums differs) to
+    1e-5; their weight gradients (through the bf16 BN-backward output, where that order can move
+    a rounding) to 2e-2. Further down the bf16 chain a one-ulp change is amplified like any bf16
+    rounding at random init (test_bf16_layerwise's docstring), so those gradients are only
+    required finite."""
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     cfg = SegConfig(height=64, width=128, nb_pp=2, pyramid="aspp")
@@ -328,22 +329,23 @@ def test_bn_fold_matches(cuda, monkeypatch):
         ctx.backward()
         torch.cuda.synchronize()
         out.append((ctx.outputs()[0].cpu().numpy().copy(), ctx.named("grads")))
-        # the folded launches really ran (blocks 3-4: two per unit) or really did not
+        # the folded launches really ran (two per bottleneck with more than 128 middle
+        # channels: block3's 6, block4's 3, the 3 adaptation units) or really did not
         n = ctx.counter("bn_fold_launches")
-        assert (n == 2 * (6 + 3)) if fold == "1" else (n == 0), (fold, n)
+        assert (n == 2 * (6 + 3 + 3)) if fold == "1" else (n == 0), (fold, n)
         ctx.close()
     (l0, g0), (l1, g1) = out
     assert np.array_equal(l0, l1)   # the forward and the loss head are untouched
-    u3 = "feature_extractor/base/resnet_v1_50/block4/unit_3/bottleneck_v1/"
-    upstream = [k for k in g0 if any(t in k for t in ("softmax_classifier", "adaptation_module",
-                                                       "pyramid_module", "extension", u3 + "conv3"))]
-    assert len(upstream) > 10
+    upstream = [k for k in g0 if k.startswith("softmax_classifier") or
+                (k.startswith("adaptation_module") and "/conv3/" in k)]
+    assert len(upstream) == 3 * 3 + 3 * 3
     for k in upstream:
         assert np.array_equal(g0[k], g1[k]), k
-    for t in ("gamma", "beta"):
-        k = u3 + "conv2/BatchNorm/" + t
-        assert _rel(g1[k], g0[k]) < 1e-5, (k, _rel(g1[k], g0[k]))
-    assert _rel(g1[u3 + "conv2/weights"], g0[u3 + "conv2/weights"]) < 2e-2
+    for head in ("l1", "l2_vehicle", "l2_human"):
+        a = f"adaptation_module/{head}_features/conv2/"
+        for t in ("gamma", "beta"):
+            assert _rel(g1[a + "BatchNorm/" + t], g0[a + "BatchNorm/" + t]) < 1e-5, (a, t)
+        assert _rel(g1[a + "weights"], g0[a + "weights"]) < 2e-2, a
     assert all(np.all(np.isfinite(v)) for v in g1.values())
 
 
