@@ -226,8 +226,8 @@ struct seg_ctx {
   std::vector<long> slab_cap;      // per conv: floats in that region
   ReduceJob* red_jobs = nullptr;   // device table, one job per deferred layer (jobs built per step)
   std::vector<ReduceJob> red_host, red_dev;   // this step's jobs / the device table's copy
-  bool defer_red_on = true;        // SEG_DEFER_REDUCE=0 at creation: off (A/B)
-  bool bq_on = false;              // SEG_BN_FOLD=1 at creation: BN-backward reduce folded (A/B)
+  bool defer_red_on = false;       // SEG_DEFER_REDUCE=1 at creation: on (A/B; -0.8 % step)
+  bool bq_on = false;              // SEG_BN_FOLD=1 at creation: BN-backward reduce folded (A/B; -1.3 %)
   bool defer_red = false;          // this step's non-stem reduces are deferred
   bool red_pending = false;        // ... and have not run yet
   float* stat_scratch = nullptr;
@@ -1290,8 +1290,10 @@ int build(seg_ctx* c) {
       tot += (size_t)c->slab_cap[li];
       tot = (tot + 63) / 64 * 64;   // 256-B aligned regions
     }
+    // off by default: the batched reduce on the compute stream cost the step more than the
+    // per-layer reduces beside the chain (-0.8 %, profiles/r05_ab_defer_fold.txt)
     const char* e = getenv("SEG_DEFER_REDUCE");
-    c->defer_red_on = !(e && e[0] == '0');
+    c->defer_red_on = e && e[0] == '1';
     const char* f = getenv("SEG_BN_FOLD");
     c->bq_on = f && f[0] == '1';
     if (int r = dalloc(c, &c->slab_all, std::max<size_t>(c->defer_red_on ? tot : 0, 64))) return r;
@@ -1965,6 +1967,10 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
 
 int seg_flush_grads(seg_ctx* c, void* stream) {
   NEED_BOUND(c);
+  // a deferred stem weight gradient may still run on the weight-gradient stream: the caller's
+  // stream waits for it (without consuming the join seg_apply_update takes), then the deferred
+  // reduces run there
+  if (int r = join_stem(c, (hipStream_t)stream, false)) return r;
   return flush_reduces(c, (hipStream_t)stream);
 }
 

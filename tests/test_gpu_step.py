@@ -208,14 +208,16 @@ def test_bf16_step_is_deterministic(cuda):
         assert np.array_equal(a["params"][k], b["params"][k]), k
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
-def test_defer_stem_update_matches(cuda, dtype):
+@pytest.mark.parametrize("dtype,defer_reduce", [("bf16", "0"), ("bf16", "1"), ("fp32", "1")])
+def test_defer_stem_update_matches(cuda, monkeypatch, dtype, defer_reduce):
     """seg_set_defer_stem (the update of every parameter but the stem's beside the stem's weight
     gradient, then the stem's; every other layer's split-K reduce deferred to one batched launch
     at the update): three steps with EMA give bitwise the same parameters, momentum and EMA
     shadows as the joined update, and the last step's gradients (read between backward and
-    update through seg_flush_grads) are bitwise the per-layer reduces'; the regulariser value (a
-    sum in another order) 1e-6."""
+    update through seg_flush_grads, which also joins the still-running stem weight gradient)
+    are bitwise the per-layer reduces'; the regulariser value (a sum in another order) 1e-6.
+    SEG_DEFER_REDUCE=1 (read at context creation) turns on the batched deferred reduces."""
+    monkeypatch.setenv("SEG_DEFER_REDUCE", defer_reduce)
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp")
