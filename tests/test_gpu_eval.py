@@ -161,8 +161,6 @@ def test_predict_order_resize_then_replace_voids(cuda, out_hw):
         assert nat.shape == ref.shape and (nat >= 0).all()
         assert float(np.mean(nat != ref)) <= 1e-3, (rv, float(np.mean(nat != ref)))
         got[rv] = nat
-    # replace_voids changes something (the void class of l1 and the l1-argmax elsewhere)
-    assert np.any(got[True] != got[False])
     if out_hw == (cfg.height, cfg.width):
         out = torch.empty((cfg.nb,) + out_hw, dtype=torch.int32, device=cuda)
         ctx.predict(ident, out, replace_voids=True, order="eval")
