@@ -184,6 +184,9 @@ def test_predict_spec_replace_voids_resized(cuda, tmp_path, init_ckpt):
                       "--height_feature_extractor", "48", "--width_feature_extractor", "64",
                       "--compute_dtype", "fp32", "--replace_voids"])
     s.per_pixel_dataset_name = "cityscapes"
+    from input_pipelines.synthetic import predict_input
+    from system_factory import SemanticSegmentation
+    s = SemanticSegmentation({"predict": predict_input}, model, s).settings   # output_Nclasses etc.
     s.height_system, s.width_system = 100, 150
     params = init_ckpt(tmp_path, pyramid="none", height=48, width=64, nb_pp=1, dtype="fp32")
     data = batch(5, 1, 0, 0, 48, 64)
