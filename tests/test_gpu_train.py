@@ -397,8 +397,8 @@ def test_train_main_c1_reference_default_shape(cuda, tmp_path, monkeypatch):
     _capture_device_losses(monkeypatch, logged)
     assert train.main(argv) == 1 and len(seen) == 1 and len(logged) == 1
     ctx = next(iter(mh._CONTEXTS.values()))
-    assert (ctx.cfg.depth, ctx.cfg.pyramid, ctx.cfg.height, ctx.cfg.width, ctx.cfg.nb_pp) == \
-        (50, "none", H, W, NPP)
+    assert (ctx.cfg.depth, ctx.cfg.height, ctx.cfg.width, ctx.cfg.nb_pp) == (50, H, W, NPP)
+    assert ctx.cfg.pyramid in (0, "none")   # seg_cfg.pyramid: 0 = no pyramid module
     logits, counts, lr = seen[0]
     assert lr == 0.01
     nat_p, nat_m, nat_e = ctx.named("params"), ctx.named("momentum"), ctx.named("ema")
