@@ -177,17 +177,17 @@ __global__ void bn_infer_finalize_all_kernel(const BnInferJob* __restrict__ jobs
 }
 
 // ---- forward apply ---------------------------------------------------------------------
-template <typename T, typename TO, int VEC>
-__global__ void bn_apply_kernel(BnApplyArgs a) {
+template <typename T, typename TO, int VEC, typename IDX>
+__device__ __forceinline__ void bn_apply_body(const BnApplyArgs& a) {
   const int cg_n = a.C / VEC;
-  const long total = a.M * cg_n;
+  const IDX total = (IDX)(a.M * cg_n);
   const T* Y = (const T*)a.y;
   const T* RES = (const T*)a.res;
   const T* Y2 = (const T*)a.y2;
   TO* O = (TO*)a.out;
-  for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
-       it += (long)gridDim.x * blockDim.x) {
-    const long m = it / cg_n;
+  for (IDX it = (IDX)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+       it += (IDX)gridDim.x * blockDim.x) {
+    const IDX m = it / (IDX)cg_n;
     const int c0 = (int)(it - m * cg_n) * VEC;
     float v[VEC];
     if constexpr (VEC == 8) {
@@ -207,8 +207,8 @@ __global__ void bn_apply_kernel(BnApplyArgs a) {
     } else if (RES) {
       size_t rm = (size_t)m;
       if (a.rs > 1) {
-        long wo = m % a.Wo;
-        long t = m / a.Wo;
+        long wo = (long)m % a.Wo;
+        long t = (long)m / a.Wo;
         long ho = t % a.Ho;
         long n = t / a.Ho;
         rm = (size_t)((n * a.Hr + ho * a.rs) * a.Wr + wo * a.rs);
@@ -226,6 +226,14 @@ __global__ void bn_apply_kernel(BnApplyArgs a) {
     if constexpr (VEC == 8) Vec8<TO>::store(O + (size_t)m * a.ldo + c0, v);
     else stf(O + (size_t)m * a.ldo + c0, v[0]);
   }
+}
+
+// generic-layout apply (the narrow logits layers: C = 14 / 7 / 3): 32-bit element indices when
+// they fit (round 5: the 64-bit division per element was most of these launches' ~10 us)
+template <typename T, typename TO, int VEC>
+__global__ void bn_apply_kernel(BnApplyArgs a) {
+  if (a.M * (a.C / VEC) < (1L << 31)) bn_apply_body<T, TO, VEC, unsigned>(a);
+  else bn_apply_body<T, TO, VEC, long>(a);
 }
 
 // ---- backward reduce: per row block partial sums of dyhat and dyhat*xhat -----------------
@@ -302,18 +310,18 @@ __global__ void bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
 }
 
-template <typename T, typename TZ, int VEC>
-__global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
+template <typename T, typename TZ, int VEC, typename IDX>
+__device__ __forceinline__ void bn_bwd_apply_body(const BnBwdArgs& a) {
   const int cg_n = a.C / VEC;
-  const long total = a.M * cg_n;
+  const IDX total = (IDX)(a.M * cg_n);
   const TZ* DZ = (const TZ*)a.dz;
   const TZ* Z = (const TZ*)a.z;
   const T* Y = (const T*)a.y;
   T* DY = (T*)a.dy;
   T* DH = (T*)a.dyhat;
-  for (long it = (long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
-       it += (long)gridDim.x * blockDim.x) {
-    const long m = it / cg_n;
+  for (IDX it = (IDX)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+       it += (IDX)gridDim.x * blockDim.x) {
+    const IDX m = it / (IDX)cg_n;
     const int c0 = (int)(it - m * cg_n) * VEC;
     float dz[VEC], y[VEC];
     if constexpr (VEC == 8) {
@@ -348,6 +356,12 @@ __global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
     if constexpr (VEC == 8) Vec8<T>::store(DY + (size_t)m * a.lddy + c0, o);
     else stf(DY + (size_t)m * a.lddy + c0, o[0]);
   }
+}
+
+template <typename T, typename TZ, int VEC>
+__global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
+  if (a.M * (a.C / VEC) < (1L << 31)) bn_bwd_apply_body<T, TZ, VEC, unsigned>(a);
+  else bn_bwd_apply_body<T, TZ, VEC, long>(a);
 }
 
 // ---- 8-channel streaming kernels (C % 8 == 0): thread -> fixed channel group ------------

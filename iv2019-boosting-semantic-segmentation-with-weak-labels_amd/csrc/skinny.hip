@@ -34,18 +34,14 @@ __global__ __launch_bounds__(SK_THREADS) void skinny_narrow_n_kernel(ConvArgs a)
   const E* X = (const E*)a.x;
   const E* Wt = (const E*)a.w;
   E* Y = (E*)a.y;
-  // weights: lane supplies W[n = lr][k = 32 kb + 8 lq .. + 8]
+  // weights: lane supplies W[n = lr][k = 32 kb + 8 lq .. + 8], one 16-B load each (rows
+  // 16-B aligned: conv_skinny_ok); round 5: these were 8 two-byte loads each, 128 per lane
+  // issued before any pixel load (the l1 logits conv 46 us for 67 MB read)
   V wv[16];
+  const V vzero = {};
 #pragma unroll
-  for (int kb = 0; kb < 16; ++kb) {
-    if (kb < nkb) {
-      E t[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        t[e] = lr < N ? Wt[(size_t)lr * a.ldw + kb * 32 + lq * 8 + e] : TypeOps<E>::from_f(0.f);
-      __builtin_memcpy(&wv[kb], t, 16);
-    }
-  }
+  for (int kb = 0; kb < 16; ++kb)
+    if (kb < nkb) wv[kb] = lr < N ? *(const V*)(Wt + (size_t)lr * a.ldw + kb * 32 + lq * 8) : vzero;
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const int r = wave * 32 + g * 16 + lr;   // row of this lane inside the tile
@@ -111,32 +107,69 @@ __global__ __launch_bounds__(SK_THREADS) void skinny_narrow_n_kernel(ConvArgs a)
   }
 }
 
+// 16-bit pair dot product with fp32 accumulation (v_dot2c_f32_bf16 / _f16)
+template <typename E> __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc);
+template <> __device__ __forceinline__ float dot2<bf16_t>(uint32_t x, uint32_t w, float acc) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2, x), __builtin_bit_cast(b2, w), acc, false);
+}
+template <> __device__ __forceinline__ float dot2<f16_t>(uint32_t x, uint32_t w, float acc) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, x), __builtin_bit_cast(h2, w), acc, false);
+}
+
 template <typename E, int K>
 __global__ __launch_bounds__(SK_THREADS) void skinny_narrow_k_kernel(ConvArgs a) {
+  constexpr int KP = K / 2;   // 16-bit pairs per row
   const long M = (long)a.N * a.Ho * a.Wo;
   const int nch = a.Co / 8;
   const int per = SK_THREADS / nch;   // rows per block step (the host picks N with nch | 256)
   const int cg = threadIdx.x % nch, rl = threadIdx.x / nch;
-  if (rl >= per) return;
   const E* X = (const E*)a.x;
-  const E* Wt = (const E*)a.w;
+  const uint16_t* Wt = (const uint16_t*)a.w;
   E* Y = (E*)a.y;
-  float w[8][K];
+  // the block's weights (Co rows of ldw 16-bit values) through LDS as packed pairs [k/2][n]:
+  // read once per block by consecutive threads, then each thread takes its 8 channels per pair
+  // as two 16-B LDS reads; the rows are v_dot2 products (two 16-bit products per instruction,
+  // fp32 accumulation). Round 5: each thread read its 8 x K weights as two-byte global loads,
+  // ~8 x K of them before its first pixel, and ran one fp32 FMA per product: the l1 logits
+  // data gradient took 76 us for 67 MB written
+  extern __shared__ uint32_t wsh[];   // [KP][Co]
+  for (int i = threadIdx.x; i < KP * a.Co; i += SK_THREADS) {
+    const int kp = i / a.Co, n = i - kp * a.Co;
+    const int k0 = 2 * kp, k1 = 2 * kp + 1;
+    const uint32_t lo = k0 < a.C ? Wt[(size_t)n * a.ldw + k0] : 0u;
+    const uint32_t hi = k1 < a.C ? Wt[(size_t)n * a.ldw + k1] : 0u;
+    wsh[i] = lo | (hi << 16);
+  }
+  __syncthreads();
+  if (rl >= per) return;
+  uint32_t w[8][KP];
 #pragma unroll
-  for (int e = 0; e < 8; ++e)
+  for (int kp = 0; kp < KP; ++kp) {
+    const uint4 lo = *(const uint4*)(wsh + kp * a.Co + cg * 8);
+    const uint4 hi = *(const uint4*)(wsh + kp * a.Co + cg * 8 + 4);
+    w[0][kp] = lo.x; w[1][kp] = lo.y; w[2][kp] = lo.z; w[3][kp] = lo.w;
+    w[4][kp] = hi.x; w[5][kp] = hi.y; w[6][kp] = hi.z; w[7][kp] = hi.w;
+  }
+  // input channels >= C (the pixel's padding up to ldx) are masked out of the products
+  uint32_t xm[KP];
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-      w[e][k] = k < a.C ? TypeOps<E>::to_f(Wt[(size_t)(cg * 8 + e) * a.ldw + k]) : 0.f;
+  for (int kp = 0; kp < KP; ++kp)
+    xm[kp] = 2 * kp + 1 < a.C ? 0xffffffffu : (2 * kp < a.C ? 0x0000ffffu : 0u);
   // rows m, m + per, m + 2 per, m + 3 per per trip: the four rows' loads go out together
   const long step = (long)gridDim.x * per * 4;
   for (long m0 = (long)blockIdx.x * per * 4 + rl; m0 < M; m0 += step) {
-    float x[4][16];
+    uint32_t x[4][KP];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const long m = m0 + (long)u * per;
       const long mc = m < M ? m : M - 1;
-      Vec8<E>::load(X + (size_t)mc * a.ldx, x[u]);
-      if constexpr (K > 8) Vec8<E>::load(X + (size_t)mc * a.ldx + 8, x[u] + 8);
+#pragma unroll
+      for (int q = 0; q < KP / 4; ++q) {
+        const uint4 v = *(const uint4*)(X + (size_t)mc * a.ldx + q * 8);
+        x[u][4 * q] = v.x; x[u][4 * q + 1] = v.y; x[u][4 * q + 2] = v.z; x[u][4 * q + 3] = v.w;
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -147,7 +180,7 @@ __global__ __launch_bounds__(SK_THREADS) void skinny_narrow_k_kernel(ConvArgs a)
       for (int e = 0; e < 8; ++e) {
         float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < K; ++k) s = __builtin_fmaf(k < a.C ? x[u][k] : 0.f, w[e][k], s);
+        for (int kp = 0; kp < KP; ++kp) s = dot2<E>(x[u][kp] & xm[kp], w[e][kp], s);
         o[e] = s;
       }
       Vec8<E>::store(Y + (size_t)m * a.ldy + cg * 8, o);
@@ -161,12 +194,14 @@ hipError_t skinny_launch(const ConvArgs& a, hipStream_t s) {
   if (a.Co <= 16) {
     hipLaunchKernelGGL(skinny_narrow_n_kernel<E>, dim3(ceil_div(M, SK_ROWS)), dim3(SK_THREADS), 0, s, a);
   } else {
-    // ~4 blocks per CU: every block loads all of its threads' weights once (scalar loads of
-    // rows K wide), so the grid stays small and each thread walks many rows
+    // ~4 blocks per CU: every block stages the weight table once, so the grid stays small and
+    // each thread walks many rows
     const int per = SK_THREADS / (a.Co / 8);
     const long blocks = std::min<long>(1024, (M + 4L * per - 1) / (4L * per));
-    if (a.C <= 8) hipLaunchKernelGGL((skinny_narrow_k_kernel<E, 8>), dim3((int)blocks), dim3(SK_THREADS), 0, s, a);
-    else hipLaunchKernelGGL((skinny_narrow_k_kernel<E, 16>), dim3((int)blocks), dim3(SK_THREADS), 0, s, a);
+    const int K = a.C <= 8 ? 8 : 16;
+    const size_t lds = (size_t)(K / 2) * a.Co * sizeof(uint32_t);
+    if (K == 8) hipLaunchKernelGGL((skinny_narrow_k_kernel<E, 8>), dim3((int)blocks), dim3(SK_THREADS), lds, s, a);
+    else hipLaunchKernelGGL((skinny_narrow_k_kernel<E, 16>), dim3((int)blocks), dim3(SK_THREADS), lds, s, a);
   }
   return hipGetLastError();
 }
@@ -177,12 +212,14 @@ bool conv_skinny_ok(int dtype, int out_f32, const ConvArgs& a) {
   if (!seg_half(dtype) || out_f32 || a.KH != 1 || a.KW != 1 || a.sf != 1 || a.st != 1 || a.pad_h ||
       a.pad_w || a.r || a.r2 || a.tap8)
     return false;
-  if (a.Co <= 16)   // narrow N: 16-B pixel loads, 4-channel stores inside ldy
+  if (a.Co <= 16)   // narrow N: 16-B pixel and weight loads, 4-channel stores inside ldy
     return a.C % 32 == 0 && a.C <= 512 && a.ldx % 8 == 0 && a.ldy >= (a.Co + 3) / 4 * 4 &&
-           a.ldy % 4 == 0;
-  // narrow K (data gradient of a narrow conv): no BN statistics
+           a.ldy % 4 == 0 && a.ldw % 8 == 0 && ((uintptr_t)a.w & 15) == 0;
+  // narrow K (data gradient of a narrow conv): no BN statistics; the weight table (K x Co fp32)
+  // fits the block's LDS
   return a.C <= 16 && a.ldx % 8 == 0 && a.ldx >= (a.C <= 8 ? 8 : 16) && a.Co % 8 == 0 &&
-         a.ldy % 8 == 0 && SK_THREADS % (a.Co / 8) == 0 && a.Co / 8 <= SK_THREADS && !a.stats;
+         a.ldy % 8 == 0 && SK_THREADS % (a.Co / 8) == 0 && a.Co / 8 <= SK_THREADS && a.Co <= 1024 &&
+         !a.stats;
 }
 
 hipError_t launch_conv_skinny(int dtype, const ConvArgs& a, hipStream_t s) {
