@@ -128,7 +128,10 @@ int seg_set_premask(seg_ctx* ctx, int on);
 /* runtime counters since seg_create (diagnostics; no reference counterpart):
  * "premask_launches" = conv1 data gradients stored pre-masked (seg_set_premask);
  * "bn_fold_launches" = data gradients whose epilogue also ran the consumer BN's backward
- * reduce (SEG_BN_FOLD=1 at seg_create). -ENOENT for an unknown name. */
+ * reduce (SEG_BN_FOLD=1 at seg_create);
+ * "lbf_layers" = conv3 layers whose BN-backward apply was folded into their data / weight
+ * gradients by linearity (16-bit identity units with an expanding conv3; SEG_LBF=0 at
+ * seg_create turns it off). -ENOENT for an unknown name. */
 int seg_counter(seg_ctx* ctx, const char* name, int64_t* value);
 
 /* outputs ------------------------------------------------------------------------------

@@ -42,6 +42,11 @@ struct BnBwdArgs {
   void* dy; int lddy;              // output gradient wrt y (T)
   void* dyhat; int lddyhat;        // optional masked gradient (T)
   const float* dzscale;            // optional per-channel factor applied to dz
+  // optional per-channel term added to dz before the gate (8-wide masked path only): the
+  // constant part of a data gradient whose producer left it out (net.cpp, linear BN-backward
+  // fold of the consumer's expansion conv)
+  const float* dshift;
+  int reduce_dyhat;                // the reduce (not the apply) stores the gated gradient in dyhat
   float* part;                     // reduce partials [rb][C][2]
   int rb;                          // number of row blocks
   // dual (launch_bn_bwd_*_dual): a second BN layer gated by the same dz and bits, e.g. a

@@ -505,11 +505,17 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
     }
   }
   __builtin_amdgcn_sched_barrier(0);   // keep the group's loads ahead of every conversion
+  float sft[8];
+  if constexpr (HS == 2) ld8(a.dshift, c0, sft);
 #pragma unroll
   for (int k = 0; k < BN_U; ++k) {
     if (FULL || k < nrows) {
       rdz[k].cvt(dz[k]);
       ry[k].cvt(y[k]);
+      if constexpr (HS == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dz[k][e] += sft[e];
+      }
       if constexpr (HZ == 1) {
         float z[8];
         rz[k].cvt(z);
@@ -524,7 +530,7 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
       for (int e = 0; e < 8; ++e) { dz[k][e] = 0.f; y[k][e] = 0.f; }
     }
   }
-  if constexpr (HS) {
+  if constexpr (HS == 1) {
     float ds[8];
     ld8(a.dzscale, c0, ds);
 #pragma unroll
@@ -535,7 +541,10 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
 }
 
 // per row block partial (sum dyhat, sum dyhat*xhat); rows of block b: [b*rows_per, ...)
-template <typename T, typename TZ, int HZ, int HS>
+// HS: 1 = dz times dzscale, 2 = dz plus dshift before the gate; HD: the gated gradient (dyhat)
+// is also stored (the linear BN-backward fold's masked gradient, read by the data and weight
+// gradients in place of the apply's output)
+template <typename T, typename TZ, int HZ, int HS, int HD = 0>
 __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
   __shared__ float sh[2][256 * 8];
   const RowLane L = row_lane(a.C / 8);
@@ -556,6 +565,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
     auto acc = [&](long base, int nrows, auto full) {
       float dz[BN_U][8], y[BN_U][8];
       bwd_load<T, TZ, HZ, HS, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
+      if constexpr (HD) {
+        T* DH = (T*)a.dyhat + c0;
+#pragma unroll
+        for (int k = 0; k < BN_U; ++k)
+          if (decltype(full)::value || k < nrows) BN_STORE8(T, DH + (size_t)(base + k * L.rpp) * a.lddyhat, dz[k]);
+      }
 #pragma unroll
       for (int k = 0; k < BN_U; ++k)
 #pragma unroll
@@ -604,19 +619,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(BnBwdArgs a) {
   T* DY = (T*)a.dy + c0;
   T* DH = (T*)a.dyhat + c0;
   float ds[8];
-  if constexpr (HS) ld8(a.dzscale, c0, ds);
+  if constexpr (HS == 1) ld8(a.dzscale, c0, ds);
   const long step = (long)L.rpp * BN_U;
   auto body = [&](long base, int nrows, auto full) {
     float dz[BN_U][8], y[BN_U][8];
     if constexpr (decltype(full)::value) nrows = BN_U;
-    bwd_load<T, TZ, HZ, 0, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
+    bwd_load<T, TZ, HZ, HS == 2 ? 2 : 0, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
 #pragma unroll
     for (int k = 0; k < BN_U; ++k) {
       if (k >= nrows) continue;
       const size_t m = (size_t)(base + k * L.rpp);
       // dyhat: the masked gradient before the per-channel factor (group norm's gamma)
       if constexpr (HD) BN_STORE8(T, DH + m * a.lddyhat, dz[k]);
-      if constexpr (HS) {
+      if constexpr (HS == 1) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) dz[k][e] *= ds[e];
       }
@@ -816,10 +831,15 @@ bool bwd_v8(const BnBwdArgs& a) {
 template <typename T, typename TZ>
 hipError_t bwd_reduce_t(const BnBwdArgs& a, hipStream_t s) {
   if (a.mask && !bwd_v8<T, TZ>(a)) return hipErrorInvalidValue;   // bits exist on the 8-wide path only
+  const bool rdh = a.reduce_dyhat && a.dyhat;
+  if ((a.dshift || rdh) && (!a.mask || a.dzscale || !bwd_v8<T, TZ>(a))) return hipErrorInvalidValue;
   if (bwd_v8<T, TZ>(a)) {
     const int cg_n = a.C / 8;
     const dim3 g(a.rb, cg_n > 256 ? ceil_div(cg_n, 256) : 1);
-    if (a.mask) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 0>), g, dim3(256), 0, s, a);
+    if (a.mask && a.dshift && rdh) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 2, 1>), g, dim3(256), 0, s, a);
+    else if (a.mask && a.dshift) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 2, 0>), g, dim3(256), 0, s, a);
+    else if (a.mask && rdh) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 0, 1>), g, dim3(256), 0, s, a);
+    else if (a.mask) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 0>), g, dim3(256), 0, s, a);
     else if (a.z && a.dzscale) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 1, 1>), g, dim3(256), 0, s, a);
     else if (a.z) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 1, 0>), g, dim3(256), 0, s, a);
     else if (a.dzscale) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 0, 1>), g, dim3(256), 0, s, a);
@@ -832,9 +852,14 @@ hipError_t bwd_reduce_t(const BnBwdArgs& a, hipStream_t s) {
 template <typename T, typename TZ>
 hipError_t bwd_apply_t(const BnBwdArgs& a, hipStream_t s) {
   if (a.mask && !bwd_v8<T, TZ>(a)) return hipErrorInvalidValue;
+  if (a.dshift && (!a.mask || a.dzscale || a.dyhat || !bwd_v8<T, TZ>(a))) return hipErrorInvalidValue;
   if (bwd_v8<T, TZ>(a)) {
     const dim3 g = grid8(a.M, a.C);
     const int key = (a.z ? 4 : 0) | (a.dzscale ? 2 : 0) | (a.dyhat ? 1 : 0);
+    if (a.dshift) {
+      hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 2, 0>), g, dim3(256), 0, s, a);
+      return hipGetLastError();
+    }
     if (a.mask) {   // ReLU bits; dzscale with them only under group norm (gamma)
       if (a.dzscale) {
         if (a.dyhat) hipLaunchKernelGGL((bn_bwd_apply8_kernel<T, TZ, 2, 1, 1>), g, dim3(256), 0, s, a);

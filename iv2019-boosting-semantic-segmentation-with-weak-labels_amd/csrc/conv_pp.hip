@@ -885,7 +885,13 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
   const int nk = p_end > p_begin ? (p_end - p_begin + PK - 1) / PK : 0;
   const int nstrips = a.Wo / PK;
 
-  const auto rs_dy = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, (int)((long)P * a.lddy * 2), 0x00020000);
+  // dy source of this tile's rows (WgradArgs::dy2: rows >= Co1 from the second source)
+  const bool sec = a.dy2 && m0 >= a.Co1;   // wave-uniform
+  const int lddy = sec ? a.lddy2 : a.lddy;
+  const int co_b = sec ? a.Co1 : 0;
+  const int co_e = a.dy2 && !sec ? a.Co1 : a.Co;
+  const auto rs_dy = __builtin_amdgcn_make_buffer_rsrc((void*)(sec ? a.dy2 : a.dy), (short)0,
+                                                       (int)((long)P * lddy * 2), 0x00020000);
   const auto rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0,
                                                       (int)((long)a.N * a.H * a.W * a.ldx * 2), 0x00020000);
 
@@ -901,7 +907,7 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
     const int i = j & 1, h = j >> 1;
     const int lc = wpp_swz(r_[i], pc);
     const int co = m0 + h * 128 + lc * 8;
-    a_voff[j] = co < a.Co ? (uint32_t)((r_[i] * a.lddy + co) * 2) : OOB;
+    a_voff[j] = co < co_e ? (uint32_t)((r_[i] * lddy + co - co_b) * 2) : OOB;
     const int col = n0 + h * 128 + lc * 8;
     const bool okc = col < Ncol;
     const int cc = okc ? col : 0;
@@ -994,7 +1000,7 @@ __device__ __forceinline__ void conv_wgrad_pp_body(const WgradArgs& a) {
       auto* ldst = (__attribute__((address_space(3))) void*)(dst + (i * 8 + wave) * 1024);
       if (hid < 2) {
         const int j = hid * 2 + i;
-        const uint32_t off = r_[i] < cur_prem ? a_voff[j] + (uint32_t)(cur_p0 * a.lddy * 2) : OOB;
+        const uint32_t off = r_[i] < cur_prem ? a_voff[j] + (uint32_t)(cur_p0 * lddy * 2) : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_dy, ldst, 16, off, 0, 0, 0);
       } else {
         const int j = (hid - 2) * 2 + i;
@@ -1203,7 +1209,8 @@ __global__ __launch_bounds__(PP_THREADS, 1) void conv_wgrad_pp_kernel(WgradArgs 
 bool conv_wgrad_pp_ok(const WgradArgs& a) {
   const long P = (long)a.N * a.Ho * a.Wo;
   return (a.C % 8) == 0 && (a.ldx % 8) == 0 && (a.Co % 8) == 0 && (a.lddy % 8) == 0 &&
-         P * a.lddy * 2 < (1L << 31) && (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31);
+         P * a.lddy * 2 < (1L << 31) && (long)a.N * a.H * a.W * a.ldx * 2 < (1L << 31) &&
+         (!a.dy2 || (a.Co1 % 256 == 0 && a.Co1 < a.Co && a.lddy2 % 8 == 0 && P * a.lddy2 * 2 < (1L << 31)));
 }
 
 hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s) {

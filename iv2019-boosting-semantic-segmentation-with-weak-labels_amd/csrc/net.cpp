@@ -14,6 +14,7 @@
 
 #include "../../include/seg_hip.h"
 #include "bn.h"
+#include "lbf.h"
 #include "input.h"
 #include "conv.h"
 #include "deconv.h"
@@ -65,6 +66,13 @@ struct ConvL {
   // ConvArgs::bq_*): per 256-row tile partials [ceil(M/256)][co][2]; nullptr = not foldable
   float* bq_part = nullptr;
   bool bq_ready = false;          // this step's partials were written by the data gradient
+  // linear BN-backward fold (lbf.h; an identity unit's expansion conv3): per-channel (A, B, D)
+  // [3][co] of the last backward, the gated gradient it read (seg_debug_tensor materialises dy
+  // from it on request: the step itself never writes dy of such a layer)
+  float* lbf_coef = nullptr;
+  bool lbf_done = false;          // folded in the last backward
+  bool lbf_dy_ready = false;      // ... and dy materialised since (seg_debug_tensor)
+  Act lbf_dyhat;
   // group norm: groups, per-image states (host copies of the device array st_dev) and the
   // forward chunk partials
   int groups = 0;
@@ -227,6 +235,22 @@ struct seg_ctx {
   ReduceJob* red_jobs = nullptr;   // device table, one job per deferred layer (jobs built per step)
   std::vector<ReduceJob> red_host, red_dev;   // this step's jobs / the device table's copy
   bool defer_red_on = false;       // SEG_DEFER_REDUCE=1 at creation: on (A/B; -0.8 % step)
+  // linear BN-backward fold (lbf.h), on unless SEG_LBF=0 at creation: 16-bit identity units
+  // whose conv3 expands (co >= 2 ci, ci > 128: blocks 3-4). Compute-stream scratch (used in
+  // order by one layer at a time): the scaled data-gradient weights, the D-scaled weights, H
+  // and its split-K slab, the data gradient's constant; weight-gradient-stream scratch: the
+  // two GEMM results and the column-sum partials of the conv input
+  bool lbf_on = false;
+  bool lbf_late = false;           // SEG_LBF_LATE=1 (A/B): side-stream work after the data gradient
+  void* lbf_wts = nullptr;
+  void* lbf_xd = nullptr;
+  void* lbf_h = nullptr;
+  float* lbf_hslab = nullptr;
+  float* lbf_bias = nullptr;
+  float* lbf_bpart = nullptr;
+  float* lbf_p1 = nullptr;
+  float* lbf_cs = nullptr;
+  int64_t lbf_launches = 0;        // layers folded (seg_counter)
   bool bq_on = false;              // SEG_BN_FOLD=1 at creation: BN-backward reduce folded (A/B; -1.3 %)
   bool defer_red = false;          // this step's non-stem reduces are deferred
   bool red_pending = false;        // ... and have not run yet
@@ -622,9 +646,13 @@ int bn_apply_one(Step& S, int li, const Act& out0, int out_f32, const Act* res0,
 int gn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const Act* dyhat_out,
                 const float* dzscale);
 
-// BN backward for layer li: dz (gradient wrt BN output), z (mask source or null)
+// BN backward for layer li: dz (gradient wrt BN output), z (mask source or null). dshift: a
+// per-channel term of dz its producer left out (added before the gate; bits only);
+// reduce_only: reduce + finalize (the linear BN-backward fold replaces the apply), the gated
+// gradient stored by the reduce when dyhat_out is given
 int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const Act* dyhat_out,
-                const float* dzscale = nullptr) {
+                const float* dzscale = nullptr, const float* dshift = nullptr,
+                bool reduce_only = false) {
   seg_ctx* c = S.c;
   if (c->gn) return gn_backward(S, li, dz, dz_f32, z, dyhat_out, dzscale);
   ConvL& L = c->convs[li];
@@ -639,6 +667,10 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   if (dyhat_out) { a.dyhat = dyhat_out->p; a.lddyhat = dyhat_out->ld; }
   a.part = L.bwd_part; a.rb = L.rb;
   a.dzscale = dzscale;
+  a.dshift = dshift;
+  a.reduce_dyhat = reduce_only && dyhat_out ? 1 : 0;
+  if ((dshift || a.reduce_dyhat) && !a.mask)
+    return set_err(&c->err, -EINVAL, "bn_backward %s: shift / reduce-side dyhat need the ReLU bits", L.name.c_str());
   const double esz = seg_half(S.dt) ? 2.0 : 4.0, zsz = dz_f32 ? 4.0 : esz;
   const double me = a.M * (double)a.C * 1e-9;
   const double gb_in = me * (zsz + (a.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
@@ -647,7 +679,7 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   const bool folded = L.bq_ready;
   L.bq_ready = false;
   if (!folded) {
-    if (int r = prof_begin(c, S.s, 4, li, gb_in, &slot)) return r;
+    if (int r = prof_begin(c, S.s, 4, li, gb_in + (a.reduce_dyhat ? me * esz : 0.0), &slot)) return r;
     HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
     if (int r = prof_end(c, S.s, slot)) return r;
   }
@@ -665,6 +697,7 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
     if (int r = sync_exchange(c, L.st.sdy, 2L * L.co, S.s)) return r;
     HIPCALL(c, launch_scale2(L.st.sdy, 2L * L.co, 1.f / c->sync_world, 0, 1.f, S.s));
   }
+  if (reduce_only) return 0;
   const double gb_apply = gb_in + me * esz * (dyhat_out ? 2 : 1);
   if (int r = prof_begin(c, S.s, 5, li, gb_apply, &slot)) return r;
   HIPCALL(c, launch_bn_bwd_apply(S.dt, dz_f32, a, S.s));
@@ -982,6 +1015,20 @@ int make_resize_grid(seg_ctx* c, GridSpec& g, int kr, int kc, int H, int W) {
 // ------------------------------------------------------------------------------------------
 // graph construction + allocation
 // ------------------------------------------------------------------------------------------
+// linear BN-backward fold (lbf.h): the unit shapes it applies to -- a 16-bit batch-norm
+// identity unit whose conv3 is an expansion 1 x 1 (co >= 2 ci) with ci > 128 (its data gradient
+// is a ping-pong launch: C2 = ci, Co = ci) and whose conv2 output gate is kept as bits
+constexpr int LBF_RB = 256;   // row blocks of the conv input's column sums
+int lbf_hsplits(const ConvL& L3) { return std::max(1, L3.co / 128); }   // H: 128 channels per split
+
+bool lbf_shape_ok(const seg_ctx* c, const Unit& u) {
+  if (!seg_half(c->dt) || c->gn || u.kind != SC_IDENTITY || u.c3 < 0 || u.c2 < 0) return false;
+  const ConvL& L3 = c->convs[u.c3];
+  const ConvL& L2 = c->convs[u.c2];
+  return L3.k == 1 && L3.stride == 1 && L3.rate == 1 && L3.co >= 2 * L3.ci && L3.ci > 128 &&
+         L3.co <= 2048 && L3.ci % 64 == 0 && L3.co % 128 == 0 && L2.co == L3.ci && L2.relu;
+}
+
 int alloc_unit(seg_ctx* c, Unit& u, const Act& in) {
   u.in = in;
   if (u.sc >= 0)
@@ -1300,6 +1347,36 @@ int build(seg_ctx* c) {
     if (int r = dalloc(c, &c->red_jobs, c->convs.size())) return r;
   }
   if (int r = dalloc(c, &c->stat_scratch, std::max<size_t>(c->stat_scratch_floats, 16))) return r;
+  {  // linear BN-backward fold: per-layer coefficients and the shared scratch (lbf.h)
+    const char* e = getenv("SEG_LBF");
+    c->lbf_on = !(e && e[0] == '0');
+    const char* el = getenv("SEG_LBF_LATE");
+    c->lbf_late = el && el[0] == '1';
+    size_t wts = 0, hh = 0, hs = 0, ci_max = 0;
+    for (auto& u : c->units) {
+      if (!lbf_shape_ok(c, u)) continue;
+      ConvL& L3 = c->convs[u.c3];
+      if (int r = dalloc(c, &L3.lbf_coef, 3 * (size_t)L3.co)) return r;
+      wts = std::max(wts, (size_t)L3.co * L3.ci);
+      hh = std::max(hh, (size_t)L3.ci * L3.ci);
+      hs = std::max(hs, (size_t)lbf_hsplits(L3) * L3.ci * L3.ci);
+      ci_max = std::max(ci_max, (size_t)L3.ci);
+    }
+    if (wts) {
+      char* p;
+      if (int r = dalloc(c, &p, wts * c->esz)) return r;
+      c->lbf_wts = p;
+      if (int r = dalloc(c, &p, wts * c->esz)) return r;
+      c->lbf_xd = p;
+      if (int r = dalloc(c, &p, hh * c->esz)) return r;
+      c->lbf_h = p;
+      if (int r = dalloc(c, &c->lbf_hslab, hs)) return r;
+      if (int r = dalloc(c, &c->lbf_bias, ci_max)) return r;
+      if (int r = dalloc(c, &c->lbf_bpart, (wts / 128) + ci_max)) return r;   // [co / 128][ci]
+      if (int r = dalloc(c, &c->lbf_p1, wts + hh)) return r;   // [P1 (co x ci) | G (ci x ci)]
+      if (int r = dalloc(c, &c->lbf_cs, (size_t)LBF_RB * ci_max)) return r;
+    }
+  }
   return 0;
 }
 
@@ -1335,6 +1412,112 @@ bool premask_ok(seg_ctx* c, const Unit& u, const Unit* pred, bool accumulate) {
   return conv_nt_omask_ok(c->dt, a);
 }
 
+// ---- linear BN-backward fold of an identity unit's conv3 (lbf.h) ----
+bool lbf_ok(seg_ctx* c, const Unit& u) {
+  if (!c->lbf_on || c->bq_on || !c->lbf_wts || !lbf_shape_ok(c, u)) return false;
+  const ConvL& L3 = c->convs[u.c3];
+  if (!L3.lbf_coef || !L3.wt_lp || !u.out.mask || u.out.C != L3.co || !u.z2.mask ||
+      u.z2.C != L3.ci || u.dz2.C != L3.ci)
+    return false;
+  ConvArgs a{};
+  a.x = u.dout.p; a.N = L3.N; a.H = L3.Ho; a.W = L3.Wo; a.C = L3.co; a.ldx = u.dout.ld;
+  a.w = c->lbf_wts; a.ldw = L3.co;
+  a.y = u.dz2.p; a.Ho = L3.H; a.Wo = L3.W; a.Co = L3.ci; a.ldy = u.dz2.ld;
+  a.x2 = u.z2.p; a.ldx2 = u.z2.ld; a.C2 = L3.ci; a.w2 = c->lbf_h; a.ldw2 = L3.ci;
+  a.KH = a.KW = 1; a.sf = 1; a.st = 1; a.dil = 1;
+  return u.dpre.ld == u.dout.ld && conv_nt_pp_ok(a);
+}
+
+// the weight gradient of a folded conv3 (on the weight-gradient stream when it is active):
+// P1 = dyhat^T y2 and G = y2^T y2 by the weight-gradient kernel, the column sums of y2, then
+// dW3 = A o P1 + B (x) colsum + D o (W3 G) into the gradient buffer
+int lbf_wgrad(Step& S, Unit& u, const Act& dyhat) {
+  seg_ctx* c = S.c;
+  const int li = u.c3;
+  ConvL& L = c->convs[li];
+  Step W = S;
+  if (c->side_active) {   // dyhat, y2 and this layer's coefficients are ready on the compute stream
+    HIPCALL(c, hipEventRecord(c->ev_dy[li], S.s));
+    HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_dy[li], 0));
+    W.s = c->side;
+  }
+  const Act& y2 = u.z2;
+  // P1 = dyhat^T y2 and G = y2^T y2 as one launch: output rows co.. co + ci - 1 take y2 as dy
+  WgradArgs a{};
+  a.dy = dyhat.p; a.lddy = dyhat.ld;
+  a.dy2 = y2.p; a.lddy2 = y2.ld; a.Co1 = L.co;
+  a.x = y2.p; a.N = y2.N; a.H = y2.H; a.W = y2.W; a.C = y2.C; a.ldx = y2.ld;
+  a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co + L.ci;
+  a.KH = a.KW = 1; a.sf = 1; a.dil = 1;
+  a.splits = wgrad_splits(a, S.dt, c->side_active);
+  a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / ((long)a.Co * a.C)));
+  a.out = c->slab;
+  if (!conv_wgrad_pp_ok(a)) return set_err(&c->err, -EINVAL, "lbf weight gradient %s: shape", L.name.c_str());
+  const long P = (long)L.N * L.Ho * L.Wo;
+  const long n1 = (long)(L.co + L.ci) * L.ci;
+  int slot;
+  // algorithmic work of the layer's weight gradient; the G rows, the column sums and the
+  // combine are time of this class too
+  const double gbx = (((double)P * L.co + (double)P * L.ci) * c->esz + (double)L.co * L.ci * 4.0) * 1e-9;
+  if (int r = prof_begin(c, W.s, 2, li, 2.0 * P * L.co * L.ci * 1e-9, &slot, gbx)) return r;
+  HIPCALL(c, launch_conv_wgrad_pp(S.dt, a, W.s));
+  HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, n1, n1, c->lbf_p1, 0, W.s));
+  HIPCALL(c, launch_lbf_colsum(S.dt, y2.p, y2.M(), y2.C, y2.ld, c->lbf_cs, LBF_RB, W.s));
+  LbfCombineArgs cb{};
+  cb.co = L.co; cb.ci = L.ci; cb.w = L.w_lp; cb.g = c->lbf_p1 + (size_t)L.co * L.ci; cb.p1 = c->lbf_p1;
+  cb.cspart = c->lbf_cs; cb.rb = LBF_RB; cb.coef = L.lbf_coef; cb.out = c->grads + L.w_off;
+  HIPCALL(c, launch_lbf_combine(S.dt, cb, W.s));
+  if (int r = prof_end(c, W.s, slot)) return r;
+  c->wg_done[li] = 1;
+  return bucket_progress(c, W.s, false);
+}
+
+// after the conv3 BN reduce + finalize: the coefficients, the scaled weights, H, the weight
+// gradient (side stream) and the conv3 data gradient as one K-concatenated GEMM
+// [dyhat | y2] x [A o W3 ; H] into u.dz2 (its constant b is left to c2's BN backward)
+int lbf_backward(Step& S, Unit& u, const Act& dyhat) {
+  seg_ctx* c = S.c;
+  ConvL& L = c->convs[u.c3];
+  const int co = L.co, ci = L.ci;
+  int slot;
+  const double gbp = (4.0 * co * ci * c->esz + (double)ci * ci * (c->esz + 4.0 * (lbf_hsplits(L) + 1))) * 1e-9;
+  if (int r = prof_begin(c, S.s, 5, u.c3, gbp, &slot)) return r;
+  LbfPrepArgs p{};
+  p.co = co; p.ci = ci;
+  p.mean = L.st.mean; p.invstd = L.st.invstd; p.scale = L.st.scale; p.sdy = L.st.sdy; p.sdyx = L.st.sdyx;
+  p.w = L.w_lp; p.wt = L.wt_lp; p.wts = c->lbf_wts; p.xd = c->lbf_xd; p.bpart = c->lbf_bpart;
+  p.coef = L.lbf_coef;
+  HIPCALL(c, launch_lbf_prep(S.dt, p, S.s));
+  if (!c->lbf_late)
+    if (int r = lbf_wgrad(S, u, dyhat)) return r;
+  WgradArgs h{};   // H[k][k'] = sum_c (D_c W3[c][k]) W3[c][k']: the channels c are the "pixels"
+  h.dy = c->lbf_xd; h.lddy = ci;
+  h.x = L.w_lp; h.N = 1; h.H = 1; h.W = co; h.C = ci; h.ldx = ci;
+  h.Ho = 1; h.Wo = co; h.Co = ci; h.KH = h.KW = 1; h.sf = 1; h.dil = 1;
+  h.splits = lbf_hsplits(L); h.out = c->lbf_hslab;
+  HIPCALL(c, launch_conv_wgrad(S.dt, h, S.s));
+  HIPCALL(c, launch_lbf_hreduce(S.dt, c->lbf_hslab, h.splits, (long)ci * ci, c->lbf_h, c->lbf_bpart,
+                                co / 128, ci, c->lbf_bias, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
+  ConvArgs a{};
+  a.x = dyhat.p; a.N = L.N; a.H = L.Ho; a.W = L.Wo; a.C = co; a.ldx = dyhat.ld;
+  a.w = c->lbf_wts; a.ldw = co;
+  a.y = u.dz2.p; a.Ho = L.H; a.Wo = L.W; a.Co = ci; a.ldy = u.dz2.ld;
+  a.x2 = u.z2.p; a.ldx2 = u.z2.ld; a.C2 = ci; a.w2 = c->lbf_h; a.ldw2 = ci;
+  a.KH = a.KW = 1; a.sf = 1; a.st = 1; a.dil = 1;
+  const long M = (long)L.N * L.H * L.W;
+  const double gbx = ((double)M * (co + ci) + (double)co * ci + (double)ci * ci + (double)M * ci) * c->esz * 1e-9;
+  if (int r = prof_begin(c, S.s, 1, u.c3, 2.0 * M * ci * co * 1e-9, &slot, gbx)) return r;
+  HIPCALL(c, launch_conv_nt_pp(S.dt, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
+  if (c->lbf_late)   // A/B: the weight gradient queued behind the data gradient
+    if (int r = lbf_wgrad(S, u, dyhat)) return r;
+  L.lbf_done = true;
+  L.lbf_dyhat = dyhat;
+  ++c->lbf_launches;
+  return 0;
+}
+
 int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred = nullptr) {
   seg_ctx* c = S.c;
   // identity / subsample shortcuts: the c3 BN backward also writes the ReLU-masked dout
@@ -1347,17 +1530,26 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred =
   const Act& dres = in_masked ? u.dout : u.dpre;   // the masked dout, wherever it lives
   const ConvL& L3 = c->convs[u.c3];
   const ConvL& Ls = c->convs[u.kind == SC_CONV ? u.sc : u.c3];
-  if (u.kind == SC_CONV && !c->gn && !c->sync_fn && u.out.mask && u.out.C == L3.co &&
-      Ls.co == L3.co && Ls.rb == L3.rb && Ls.y.M() == L3.y.M()) {
-    if (int r = bn_backward_dual(S, u.c3, u.sc, u.dout, u.out)) return r;
+  const bool lbf = lbf_ok(c, u);
+  if (lbf) {
+    // linear BN-backward fold: reduce + finalize of conv3's BN (the gated gradient into dpre
+    // by the reduce itself when dout is not pre-masked), then no apply pass (lbf_backward)
+    if (int r = bn_backward(S, u.c3, u.dout, 0, in_masked ? nullptr : &u.out, dpre, nullptr, nullptr, true))
+      return r;
+    if (int r = lbf_backward(S, u, dres)) return r;
   } else {
-    if (int r = bn_backward(S, u.c3, u.dout, 0, in_masked ? nullptr : &u.out, dpre)) return r;
-    if (u.kind == SC_CONV)
-      if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
+    if (u.kind == SC_CONV && !c->gn && !c->sync_fn && u.out.mask && u.out.C == L3.co &&
+        Ls.co == L3.co && Ls.rb == L3.rb && Ls.y.M() == L3.y.M()) {
+      if (int r = bn_backward_dual(S, u.c3, u.sc, u.dout, u.out)) return r;
+    } else {
+      if (int r = bn_backward(S, u.c3, u.dout, 0, in_masked ? nullptr : &u.out, dpre)) return r;
+      if (u.kind == SC_CONV)
+        if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
+    }
+    if (int r = conv_wgrad(S, u.c3, u.z2)) return r;
+    if (int r = conv_dgrad(S, u.c3, u.dz2, nullptr, nullptr, nullptr, u.c2, &u.z2)) return r;
   }
-  if (int r = conv_wgrad(S, u.c3, u.z2)) return r;
-  if (int r = conv_dgrad(S, u.c3, u.dz2, nullptr, nullptr, nullptr, u.c2, &u.z2)) return r;
-  if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr)) return r;
+  if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr, nullptr, lbf ? c->lbf_bias : nullptr)) return r;
   if (int r = conv_wgrad(S, u.c2, u.z1)) return r;
   if (int r = conv_dgrad(S, u.c2, u.dz1, nullptr, nullptr, nullptr, u.c1, &u.z1)) return r;
   if (int r = bn_backward(S, u.c1, u.dz1, 0, &u.z1, nullptr)) return r;
@@ -1547,6 +1739,7 @@ int backward_layers(Step& S) {
   // no pre-masked gradient survives a backward that stopped part-way (unit_backward)
   for (auto& u : c->units) u.dout_masked = false;
   for (auto& u : c->heads) u.dout_masked = false;
+  for (auto& L : c->convs) L.lbf_done = L.lbf_dy_ready = false;
   // hybrid: the loss-normalised gradient goes back through the deconvolution first (its
   // weight / bias gradients and dx), then into the logits BN without a further scale
   if (c->hybrid) HIPCALL(c, launch_deconv_bwd(deconv_args(c), S.s));
@@ -1991,6 +2184,7 @@ int seg_counter(seg_ctx* c, const char* name, int64_t* value) {
   const std::string n(name);
   if (n == "premask_launches") *value = c->premask_launches;
   else if (n == "bn_fold_launches") *value = c->bq_launches;
+  else if (n == "lbf_layers") *value = c->lbf_launches;
   else return set_err(&c->err, -ENOENT, "unknown counter '%s'", name);
   return 0;
 }
@@ -2179,7 +2373,27 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
       a.p = c->img_dbg; a.N = st.N; a.H = st.H; a.W = st.W; a.C = 3; a.ld = 8;
     } else if (n.substr(us) == "_x") a = c->convs[i].x;
     else if (n.substr(us) == "_y") a = c->convs[i].y;
-    else if (n.substr(us) == "_dy") a = c->convs[i].dy;
+    else if (n.substr(us) == "_dy") {
+      ConvL& L = c->convs[i];
+      if (L.lbf_done && !L.lbf_dy_ready) {   // folded (lbf.h): the step never wrote it; the apply it replaced, now
+        HIPCALL(c, hipDeviceSynchronize());
+        BnBwdArgs b{};
+        b.dz = L.lbf_dyhat.p; b.lddz = L.lbf_dyhat.ld;
+        b.y = L.y.p; b.ldy = L.y.ld; b.M = L.y.M(); b.C = L.co;
+        b.mean = L.st.mean; b.invstd = L.st.invstd; b.scale = L.st.scale;
+        b.sdy = L.st.sdy; b.sdyx = L.st.sdyx;
+        b.dy = L.dy.p; b.lddy = L.dy.ld;
+        HIPCALL(c, launch_bn_bwd_apply(c->dt, 0, b, nullptr));
+        HIPCALL(c, hipDeviceSynchronize());
+        L.lbf_dy_ready = true;
+      }
+      a = L.dy;
+    }
+    else if (n.substr(us) == "_dyhat" && c->convs[i].lbf_done) a = c->convs[i].lbf_dyhat;
+    else if (n.substr(us) == "_lbfcoef" && c->convs[i].lbf_done) {   // [3][co] = A, B, D (lbf.h)
+      a.p = c->convs[i].lbf_coef; a.N = 1; a.H = 1; a.W = 3; a.C = a.ld = c->convs[i].co;
+      dt = SEG_DTYPE_F32;
+    }
     else return set_err(&c->err, -EINVAL, "unknown tensor %s", name);
   } else {
     return set_err(&c->err, -EINVAL, "unknown tensor %s", name);

@@ -351,6 +351,56 @@ def test_bn_fold_matches(cuda, monkeypatch):
     assert all(np.all(np.isfinite(v)) for v in g1.values())
 
 
+def test_lbf_matches(cuda, monkeypatch):
+    """Linear BN-backward fold (round 5, csrc/lbf.h): the conv3 BN-backward apply of the 16-bit
+    identity units with an expanding conv3 (block3 units 2-6, block4 units 2-3 of R50) is
+    replaced by the affine form dz3 = A dyhat + B + D z3 pushed through the data gradient
+    ([dyhat | y2] x [A o W3 ; W3^T diag(D) W3], constant added by conv2's BN backward) and the
+    weight gradient (A o dyhat^T y2 + B colsum(y2) + D o W3 y2^T y2). Against SEG_LBF=0 on the
+    same inputs: the forward and loss bitwise, every gradient the backward computes before the
+    first folded layer bitwise (the heads, the pyramid, decrease_fdims), the first folded
+    layer's BN gamma / beta bitwise (its reduce is unchanged), its weight gradient and its conv2
+    BN gradients to the rounding the two orders differ by; the rest finite. The counter says
+    which layers folded. Parity of the folded layers against the float64 oracle chain:
+    tests/test_gpu_fullsize.py (conv3 -> conv2 data gradients, conv3 weight gradients)."""
+    from input_pipelines.synthetic import batch
+    from seg_hip import SegContext
+    cfg = SegConfig(height=64, width=128, nb_pp=2, pyramid="aspp")
+    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=14).items()}
+    data = batch(25, cfg.nb_pp, 0, 0, cfg.height, cfg.width)
+    img = torch.as_tensor(data["images"]).to(cuda)
+    px = torch.as_tensor(data["px"]).to(cuda)
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("SEG_LBF", on)   # read at context creation
+        ctx = SegContext(pyramid=cfg.pyramid, height=cfg.height, width=cfg.width, nb_pp=2,
+                         dtype="bf16")
+        ctx.load_params(params)
+        ctx.forward(img)
+        ctx.loss(px, None, None)
+        ctx.backward()
+        torch.cuda.synchronize()
+        out.append((ctx.outputs()[0].cpu().numpy().copy(), ctx.named("grads")))
+        n = ctx.counter("lbf_layers")
+        assert n == (5 + 2 if on == "1" else 0), (on, n)
+        ctx.close()
+    (l0, g0), (l1, g1) = out
+    assert np.array_equal(l0, l1)
+    first = "feature_extractor/base/resnet_v1_50/block4/unit_3/bottleneck_v1/"
+    upstream = [k for k in g0 if not k.startswith("feature_extractor/base/")]
+    assert len(upstream) > 20
+    for k in upstream:
+        assert np.array_equal(g0[k], g1[k]), k
+    for t in ("gamma", "beta"):
+        assert np.array_equal(g0[first + "conv3/BatchNorm/" + t], g1[first + "conv3/BatchNorm/" + t])
+    d_w3 = _rel(g1[first + "conv3/weights"], g0[first + "conv3/weights"])
+    d_g2 = _rel(g1[first + "conv2/BatchNorm/gamma"], g0[first + "conv2/BatchNorm/gamma"])
+    d_b2 = _rel(g1[first + "conv2/BatchNorm/beta"], g0[first + "conv2/BatchNorm/beta"])
+    print(f"lbf: conv3 weights {d_w3:.3e}, conv2 gamma {d_g2:.3e}, beta {d_b2:.3e}")
+    assert d_w3 < 1e-2 and d_g2 < 2e-2 and d_b2 < 2e-2, (d_w3, d_g2, d_b2)
+    assert all(np.all(np.isfinite(v)) for v in g1.values())
+
+
 def test_defer_stem_join_on_other_stream(cuda):
     """with defer on, a join-taking call on another stream (seg_predict on B) between
     seg_backward and seg_apply_update (both on A) must not consume the pending stem join: the
