@@ -28,7 +28,7 @@ struct ConvArgs {
   float* stats;   // BN partials [mtiles][Co] x {sum, M2} (nullptr = none)
   int tap8;       // tap mode: a tap is tap8 16-B chunks of K (2: the space-to-depth stem, 16
                   // channels per tap); K = KH*KW*C is padded to a multiple of 64 with zero weights
-  // K-concatenated second GEMM (ping-pong dense 1x1 path only): y = x w^T + x2 w2^T, x2 [..][ldx2]
+  // K-concatenated second GEMM (dense 1x1: the ping-pong path, and v2 for Co <= 128): y = x w^T + x2 w2^T, x2 [..][ldx2]
   // with C2 channels on the same pixels, w2 [Co][ldw2]; a projection unit's conv1 + shortcut
   // data gradients into the unit input in one accumulation (x2 = nullptr: single GEMM)
   const void* x2;
@@ -93,6 +93,9 @@ int conv_nt_v2_rows(const ConvArgs& a);   // tile rows (= BN-stat partial rows) 
 // true when launch_conv_nt runs the v2 kernel
 bool conv_nt_uses_v2(int dtype, int out_f32, const ConvArgs& a);
 hipError_t launch_conv_nt_v2(int dtype, const ConvArgs& a, hipStream_t s);
+// the v2 kernel's K-concatenated second GEMM (ConvArgs::x2): dense 1x1, stride 1, Co <= 128, no
+// residual or statistics (launch_conv_nt_v2 takes it when x2 is set)
+bool conv_nt_v2_dual_ok(const ConvArgs& a);
 // skinny 1x1 convs (skinny.hip): N <= 16 (the logits convs, with BN partials per 128 rows) or
 // K <= 16 (their data gradients), 16-bit storage; taken where the v2 kernels cannot run
 bool conv_skinny_ok(int dtype, int out_f32, const ConvArgs& a);

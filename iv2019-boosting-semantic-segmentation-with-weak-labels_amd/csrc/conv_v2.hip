@@ -65,7 +65,10 @@ template <> struct AccOf<16> { typedef f32x4_t T; static constexpr int N = 4; };
 // MF: MFMA shape (16: v_mfma_f32_16x16x32_bf16). A v_mfma_f32_32x32x16_bf16 main loop with
 // fragments double-buffered across k16-steps was measured 5-9 % slower on the C2 layer shapes
 // and removed; the epilogue keeps the shape-generic (row_of / col_of) accumulator walk.
-template <typename E, int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM_ = 256>
+// DU: dense 1x1 rows plus a K-concatenated second GEMM (x2, w2), the ping-pong kernel's ST = 4
+// for output tiles of <= 128 channels (csrc/lbf.h: the folded conv3 data gradient of block1-2)
+template <typename E, int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM_ = 256,
+          int DU = 0>
 __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_kernel(ConvArgs a) {
   typedef typename Half<E>::V V;
   const E* zero = (const E*)g_zero16;
@@ -104,7 +107,8 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
   const long m0 = (long)mt * BM;
   const int n0 = nt * BN;
   const int K = a.KH * a.KW * a.C;
-  const int nk = T8 ? (K + BK - 1) / BK : K / BK;   // tap mode: taps beyond KH*KW read zeros
+  const int nk1 = T8 ? (K + BK - 1) / BK : K / BK;   // tap mode: taps beyond KH*KW read zeros
+  const int nk = nk1 + (DU ? a.C2 / BK : 0);
   const E* X = (const E*)a.x;
   const E* Wt = (const E*)a.w;
 
@@ -137,6 +141,19 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
   const int ntaps = a.KH * a.KW;
   auto kcol = [&](int kb) { return T8 ? kb * BK : (kb % ntaps) * a.C + (kb / ntaps) * BK; };
   auto issue_a = [&](int kb, int stage) {
+    if constexpr (DU) {   // the second GEMM's K-steps: the same pixels of x2 (dense 1x1)
+      if (kb >= nk1) {
+        char* sA = smem + stage * STAGE_BYTES;
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          const int lc = swz(a_row[i], pc);
+          const bool ok = a_h0[i] >= 0;
+          const size_t off = ((size_t)(a_nb[i] + a_h0[i]) * a.W + a_w0[i]) * a.ldx2 + (kb - nk1) * BK + lc * 8;
+          glds16(ok ? (const void*)((const E*)a.x2 + off) : (const void*)zero, sA + (i * 8 + wave) * 1024);
+        }
+        return;
+      }
+    }
     const int tap = T8 ? 0 : kb % ntaps;
     const int c0 = T8 ? 0 : (kb / ntaps) * BK;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
@@ -170,14 +187,17 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
     }
   };
   auto issue_b = [&](int kb, int stage) {
-    const int k0 = kcol(kb);
+    const bool sec = DU && kb >= nk1;
+    const int k0 = sec ? (kb - nk1) * BK : kcol(kb);
+    const E* Wb = sec ? (const E*)a.w2 : Wt;
+    const int ldw = sec ? a.ldw2 : a.ldw;
     char* sB = smem + stage * STAGE_BYTES + BM * 128;
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int row = (i * 8 + wave) * 8 + (lane >> 3);
       const int co = n0 + row;
       const int lc = swz(row, pc);
-      const E* src = co < a.Co ? Wt + (size_t)co * a.ldw + k0 + lc * 8 : zero;
+      const E* src = co < a.Co ? Wb + (size_t)co * ldw + k0 + lc * 8 : zero;
       glds16(src, sB + (i * 8 + wave) * 1024);
     }
   };
@@ -423,13 +443,14 @@ __global__ __launch_bounds__(V2_THREADS, BM_ == 256 ? 1 : 2) void conv_nt_v2_ker
   }
 }
 
-template <typename E, int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM = 256>
+template <typename E, int BN, int WMW, int WNW, int STAGES, int ST, int T8 = 0, int MF = 16, int BM = 256,
+          int DU = 0>
 hipError_t v2_launch(const ConvArgs& a, hipStream_t s) {
   constexpr int STAGE_BYTES = (BM + BN) * 128;
   constexpr int EPI = BM * (64 + 4) * 4;
   constexpr int LDS = STAGES * STAGE_BYTES > EPI ? STAGES * STAGE_BYTES : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = conv_nt_v2_kernel<E, BN, WMW, WNW, STAGES, ST, T8, MF, BM>;
+  auto kern = conv_nt_v2_kernel<E, BN, WMW, WNW, STAGES, ST, T8, MF, BM, DU>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -878,8 +899,22 @@ int conv_nt_v2_rows(const ConvArgs& a) {
   return v2_small_tile(a) ? 128 : 256;
 }
 
+// K-concatenated second GEMM on output tiles of <= 128 channels (dense 1x1 rows only)
+bool conv_nt_v2_dual_ok(const ConvArgs& a) {
+  return a.x2 && a.st == 1 && a.sf == 1 && a.KH == 1 && a.KW == 1 && a.pad_h == 0 && a.pad_w == 0 &&
+         a.H == a.Ho && a.W == a.Wo && a.Co <= 128 && a.C2 % BK == 0 && a.ldx2 % 8 == 0 &&
+         a.ldw2 % 8 == 0 && !a.r && !a.r2 && !a.stats && !a.tap8;
+}
+
 template <typename E, int ST>
 hipError_t v2_dispatch(int dtype, const ConvArgs& a, hipStream_t s) {
+  if constexpr (ST == 1) {
+    if (a.x2) {
+      if (!conv_nt_v2_dual_ok(a) || !conv_nt_v2_ok(a)) return hipErrorInvalidValue;
+      if (a.Co > 64) return v2_launch<E, 128, 4, 2, 3, 1, 0, 16, 256, 1>(a, s);
+      return v2_launch<E, 64, 8, 1, 3, 1, 0, 16, 128, 1>(a, s);
+    }
+  }
   if (ST == 1 && conv_nt_patch_ok(a)) {
     // 64-channel output tiles with one patch buffer fit 72 KB and 110 VGPRs: two workgroups
     // per CU hide each other's barrier and fragment-read latency (a 128-channel tile at two

@@ -1016,16 +1016,20 @@ int make_resize_grid(seg_ctx* c, GridSpec& g, int kr, int kc, int H, int W) {
 // graph construction + allocation
 // ------------------------------------------------------------------------------------------
 // linear BN-backward fold (lbf.h): the unit shapes it applies to -- a 16-bit batch-norm
-// identity unit whose conv3 is an expansion 1 x 1 (co >= 2 ci) with ci > 128 (its data gradient
-// is a ping-pong launch: C2 = ci, Co = ci) and whose conv2 output gate is kept as bits
+// identity unit whose conv3 is an expansion 1 x 1 (co >= 2 ci, ci a multiple of 64; its data
+// gradient is a ping-pong launch for ci > 128, a v2 launch otherwise: C2 = ci, Co = ci) and whose
+// conv2 output gate is kept as bits
 constexpr int LBF_RB = 256;   // row blocks of the conv input's column sums
+#ifndef LBF_MIN_CI
+#define LBF_MIN_CI 64   // A/B builds: 256 = block3-4 only (the first version)
+#endif
 int lbf_hsplits(const ConvL& L3) { return std::max(1, L3.co / 128); }   // H: 128 channels per split
 
 bool lbf_shape_ok(const seg_ctx* c, const Unit& u) {
   if (!seg_half(c->dt) || c->gn || u.kind != SC_IDENTITY || u.c3 < 0 || u.c2 < 0) return false;
   const ConvL& L3 = c->convs[u.c3];
   const ConvL& L2 = c->convs[u.c2];
-  return L3.k == 1 && L3.stride == 1 && L3.rate == 1 && L3.co >= 2 * L3.ci && L3.ci > 128 &&
+  return L3.k == 1 && L3.stride == 1 && L3.rate == 1 && L3.co >= 2 * L3.ci && L3.ci >= LBF_MIN_CI &&
          L3.co <= 2048 && L3.ci % 64 == 0 && L3.co % 128 == 0 && L2.co == L3.ci && L2.relu;
 }
 
@@ -1425,7 +1429,8 @@ bool lbf_ok(seg_ctx* c, const Unit& u) {
   a.y = u.dz2.p; a.Ho = L3.H; a.Wo = L3.W; a.Co = L3.ci; a.ldy = u.dz2.ld;
   a.x2 = u.z2.p; a.ldx2 = u.z2.ld; a.C2 = L3.ci; a.w2 = c->lbf_h; a.ldw2 = L3.ci;
   a.KH = a.KW = 1; a.sf = 1; a.st = 1; a.dil = 1;
-  return u.dpre.ld == u.dout.ld && conv_nt_pp_ok(a);
+  if (u.dpre.ld != u.dout.ld) return false;
+  return L3.ci > 128 ? conv_nt_pp_ok(a) : conv_nt_v2_ok(a) && conv_nt_v2_dual_ok(a);
 }
 
 // the weight gradient of a folded conv3 (on the weight-gradient stream when it is active):
@@ -1442,17 +1447,6 @@ int lbf_wgrad(Step& S, Unit& u, const Act& dyhat) {
     W.s = c->side;
   }
   const Act& y2 = u.z2;
-  // P1 = dyhat^T y2 and G = y2^T y2 as one launch: output rows co.. co + ci - 1 take y2 as dy
-  WgradArgs a{};
-  a.dy = dyhat.p; a.lddy = dyhat.ld;
-  a.dy2 = y2.p; a.lddy2 = y2.ld; a.Co1 = L.co;
-  a.x = y2.p; a.N = y2.N; a.H = y2.H; a.W = y2.W; a.C = y2.C; a.ldx = y2.ld;
-  a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co + L.ci;
-  a.KH = a.KW = 1; a.sf = 1; a.dil = 1;
-  a.splits = wgrad_splits(a, S.dt, c->side_active);
-  a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / ((long)a.Co * a.C)));
-  a.out = c->slab;
-  if (!conv_wgrad_pp_ok(a)) return set_err(&c->err, -EINVAL, "lbf weight gradient %s: shape", L.name.c_str());
   const long P = (long)L.N * L.Ho * L.Wo;
   const long n1 = (long)(L.co + L.ci) * L.ci;
   int slot;
@@ -1460,8 +1454,35 @@ int lbf_wgrad(Step& S, Unit& u, const Act& dyhat) {
   // combine are time of this class too
   const double gbx = (((double)P * L.co + (double)P * L.ci) * c->esz + (double)L.co * L.ci * 4.0) * 1e-9;
   if (int r = prof_begin(c, W.s, 2, li, 2.0 * P * L.co * L.ci * 1e-9, &slot, gbx)) return r;
-  HIPCALL(c, launch_conv_wgrad_pp(S.dt, a, W.s));
-  HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, n1, n1, c->lbf_p1, 0, W.s));
+  if (L.ci < 256) {   // narrow ci: P1 and G as two weight-gradient launches of their own tile shapes
+    for (int part = 0; part < 2; ++part) {
+      WgradArgs a{};
+      a.dy = part ? y2.p : dyhat.p; a.lddy = part ? y2.ld : dyhat.ld;
+      a.x = y2.p; a.N = y2.N; a.H = y2.H; a.W = y2.W; a.C = y2.C; a.ldx = y2.ld;
+      a.Ho = L.Ho; a.Wo = L.Wo; a.Co = part ? L.ci : L.co;
+      a.KH = a.KW = 1; a.sf = 1; a.dil = 1;
+      const long n = (long)a.Co * a.C;
+      a.splits = wgrad_splits(a, S.dt, c->side_active);
+      a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / n));
+      a.out = c->slab;
+      HIPCALL(c, launch_conv_wgrad(S.dt, a, W.s));
+      HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, n, n, c->lbf_p1 + (part ? (size_t)L.co * L.ci : 0), 0, W.s));
+    }
+  } else {
+    // P1 = dyhat^T y2 and G = y2^T y2 as one launch: output rows co.. co + ci - 1 take y2 as dy
+    WgradArgs a{};
+    a.dy = dyhat.p; a.lddy = dyhat.ld;
+    a.dy2 = y2.p; a.lddy2 = y2.ld; a.Co1 = L.co;
+    a.x = y2.p; a.N = y2.N; a.H = y2.H; a.W = y2.W; a.C = y2.C; a.ldx = y2.ld;
+    a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co + L.ci;
+    a.KH = a.KW = 1; a.sf = 1; a.dil = 1;
+    a.splits = wgrad_splits(a, S.dt, c->side_active);
+    a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / ((long)a.Co * a.C)));
+    a.out = c->slab;
+    if (!conv_wgrad_pp_ok(a)) return set_err(&c->err, -EINVAL, "lbf weight gradient %s: shape", L.name.c_str());
+    HIPCALL(c, launch_conv_wgrad_pp(S.dt, a, W.s));
+    HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, n1, n1, c->lbf_p1, 0, W.s));
+  }
   HIPCALL(c, launch_lbf_colsum(S.dt, y2.p, y2.M(), y2.C, y2.ld, c->lbf_cs, LBF_RB, W.s));
   LbfCombineArgs cb{};
   cb.co = L.co; cb.ci = L.ci; cb.w = L.w_lp; cb.g = c->lbf_p1 + (size_t)L.co * L.ci; cb.p1 = c->lbf_p1;
@@ -1480,16 +1501,22 @@ int lbf_backward(Step& S, Unit& u, const Act& dyhat) {
   ConvL& L = c->convs[u.c3];
   const int co = L.co, ci = L.ci;
   int slot;
-  const double gbp = (4.0 * co * ci * c->esz + (double)ci * ci * (c->esz + 4.0 * (lbf_hsplits(L) + 1))) * 1e-9;
-  if (int r = prof_begin(c, S.s, 5, u.c3, gbp, &slot)) return r;
+  // profiled as BN-backward apply time (the pass they replace), in two records so that the
+  // weight gradient queued between them (one stream when profiling) is not counted twice:
+  // the prep's bytes (both weight copies read and written), then H's (its operands, slab and
+  // 16-bit result)
+  if (int r = prof_begin(c, S.s, 5, u.c3, 4.0 * co * ci * c->esz * 1e-9, &slot)) return r;
   LbfPrepArgs p{};
   p.co = co; p.ci = ci;
   p.mean = L.st.mean; p.invstd = L.st.invstd; p.scale = L.st.scale; p.sdy = L.st.sdy; p.sdyx = L.st.sdyx;
   p.w = L.w_lp; p.wt = L.wt_lp; p.wts = c->lbf_wts; p.xd = c->lbf_xd; p.bpart = c->lbf_bpart;
   p.coef = L.lbf_coef;
   HIPCALL(c, launch_lbf_prep(S.dt, p, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
   if (!c->lbf_late)
     if (int r = lbf_wgrad(S, u, dyhat)) return r;
+  const double gbh = (2.0 * co * ci * c->esz + (double)ci * ci * (c->esz + 8.0 * lbf_hsplits(L))) * 1e-9;
+  if (int r = prof_begin(c, S.s, 5, u.c3, gbh, &slot)) return r;
   WgradArgs h{};   // H[k][k'] = sum_c (D_c W3[c][k]) W3[c][k']: the channels c are the "pixels"
   h.dy = c->lbf_xd; h.lddy = ci;
   h.x = L.w_lp; h.N = 1; h.H = 1; h.W = co; h.C = ci; h.ldx = ci;
@@ -1508,7 +1535,8 @@ int lbf_backward(Step& S, Unit& u, const Act& dyhat) {
   const long M = (long)L.N * L.H * L.W;
   const double gbx = ((double)M * (co + ci) + (double)co * ci + (double)ci * ci + (double)M * ci) * c->esz * 1e-9;
   if (int r = prof_begin(c, S.s, 1, u.c3, 2.0 * M * ci * co * 1e-9, &slot, gbx)) return r;
-  HIPCALL(c, launch_conv_nt_pp(S.dt, a, S.s));
+  if (ci > 128) HIPCALL(c, launch_conv_nt_pp(S.dt, a, S.s));
+  else HIPCALL(c, launch_conv_nt_v2(S.dt, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
   if (c->lbf_late)   // A/B: the weight gradient queued behind the data gradient
     if (int r = lbf_wgrad(S, u, dyhat)) return r;

@@ -11,5 +11,5 @@ with open(sys.argv[2], "w") as f:
     f.write("start_us,dur_us,stream,name\n")
     for n, s, q, a, b in rows:
         if t0 <= a < t1:
-            short = n.split("(")[0].replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "")
+            short = n.replace("void ", "", 1).replace("(anonymous namespace)::", "").split("(")[0]
             f.write("%.2f,%.2f,%d,%s\n" % ((a - t0) / 1e3, (b - a) / 1e3, s, short.replace(",", ";")))
