@@ -126,7 +126,8 @@ int seg_flush_grads(seg_ctx* ctx, void* stream);
  * No reference counterpart. */
 int seg_set_premask(seg_ctx* ctx, int on);
 /* runtime counters since seg_create (diagnostics; no reference counterpart):
- * "premask_launches" = conv1 data gradients stored pre-masked (seg_set_premask);
+ * "premask_launches" = data gradients stored pre-masked (seg_set_premask): identity units'
+ *   conv1, and at block boundaries a projection unit's conv1 + shortcut and decrease_fdims';
  * "bn_fold_launches" = data gradients whose epilogue also ran the consumer BN's backward
  * reduce (SEG_BN_FOLD=1 at seg_create);
  * "lbf_layers" = conv3 layers whose BN-backward apply was folded into their data / weight

@@ -47,6 +47,11 @@ struct BnBwdArgs {
   // fold of the consumer's expansion conv)
   const float* dshift;
   int reduce_dyhat;                // the reduce (not the apply) stores the gated gradient in dyhat
+  // optional (8-wide masked reduce with dshift): per row block column sums of the forward
+  // output relu((y - mean) * scale + beta) rounded to T as the forward BN apply stored it,
+  // recomputed from y, [rb][C] (the linear BN-backward fold's colsum of the next conv's input)
+  const float* beta;
+  float* cs_part;
   float* part;                     // reduce partials [rb][C][2]
   int rb;                          // number of row blocks
   // dual (launch_bn_bwd_*_dual): a second BN layer gated by the same dz and bits, e.g. a

@@ -544,9 +544,11 @@ __device__ __forceinline__ void bwd_load(const BnBwdArgs& a, int c0, long base, 
 // HS: 1 = dz times dzscale, 2 = dz plus dshift before the gate; HD: the gated gradient (dyhat)
 // is also stored (the linear BN-backward fold's masked gradient, read by the data and weight
 // gradients in place of the apply's output)
-template <typename T, typename TZ, int HZ, int HS, int HD = 0>
+// CS: also the column sums of the forward output (BnBwdArgs::cs_part), recomputed per element
+// exactly as bn_apply8_kernel forms it (fma, ReLU, rounding to T)
+template <typename T, typename TZ, int HZ, int HS, int HD = 0, int CS = 0>
 __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
-  __shared__ float sh[2][256 * 8];
+  __shared__ float sh[CS ? 3 : 2][256 * 8];
   const RowLane L = row_lane(a.C / 8);
   const int c0 = (L.act ? L.cg : 0) * 8;
   const long rows_per = (a.M + a.rb - 1) / a.rb;
@@ -556,12 +558,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
   // one accumulator set per row slot k: the U rows of a group stay independent (no loop
   // rerolling), so their loads are issued together
   float t1[BN_U][8], t2[BN_U][8];
+  float s3[8], fsc[8], fbe[8];
 #pragma unroll
   for (int k = 0; k < BN_U; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e) { t1[k][e] = 0.f; t2[k][e] = 0.f; }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s3[e] = 0.f;
   if (L.act) {
     ld8(a.mean, c0, mu); ld8(a.invstd, c0, inv);
+    if constexpr (CS) { ld8(a.scale, c0, fsc); ld8(a.beta, c0, fbe); }
     auto acc = [&](long base, int nrows, auto full) {
       float dz[BN_U][8], y[BN_U][8];
       bwd_load<T, TZ, HZ, HS, decltype(full)::value>(a, c0, base, L.rpp, nrows, dz, y);
@@ -578,6 +584,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
           t1[k][e] += dz[k][e];
           t2[k][e] += dz[k][e] * ((y[k][e] - mu[e]) * inv[e]);
         }
+      if constexpr (CS) {   // rows past the block are zero in y: skip them, not their value
+#pragma unroll
+        for (int k = 0; k < BN_U; ++k)
+          if (decltype(full)::value || k < nrows)
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              s3[e] += TypeOps<T>::to_f(TypeOps<T>::from_f(fmaxf(__builtin_fmaf(y[k][e] - mu[e], fsc[e], fbe[e]), 0.f)));
+      }
     };
     long base = r0 + L.rl;
     for (; base + (BN_U - 1) * L.rpp < r1; base += (long)L.rpp * BN_U) acc(base, BN_U, std::true_type{});
@@ -592,6 +606,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
   for (int e = 0; e < 8; ++e) {
     sh[0][threadIdx.x * 8 + e] = s1[e];
     sh[1][threadIdx.x * 8 + e] = s2[e];
+    if constexpr (CS) sh[CS ? 2 : 0][threadIdx.x * 8 + e] = s3[e];
   }
   __syncthreads();
   if (L.act && L.rl == 0) {
@@ -599,12 +614,20 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce8_kernel(BnBwdArgs a) {
     for (int r = 1; r < L.rpp; ++r) {
       const int t = r * cg_b + threadIdx.x;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { s1[e] += sh[0][t * 8 + e]; s2[e] += sh[1][t * 8 + e]; }
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += sh[0][t * 8 + e]; s2[e] += sh[1][t * 8 + e];
+        if constexpr (CS) s3[e] += sh[CS ? 2 : 0][t * 8 + e];
+      }
     }
     float* o = a.part + 2 * ((size_t)blockIdx.x * a.C + c0);
 #pragma unroll
     for (int e = 0; e < 8; e += 2)
       *(float4*)(o + 2 * e) = make_float4(s1[e], s2[e], s1[e + 1], s2[e + 1]);
+    if constexpr (CS) {
+      float* q = a.cs_part + (size_t)blockIdx.x * a.C + c0;
+      *(float4*)q = make_float4(s3[0], s3[1], s3[2], s3[3]);
+      *(float4*)(q + 4) = make_float4(s3[4], s3[5], s3[6], s3[7]);
+    }
   }
 }
 
@@ -833,10 +856,12 @@ hipError_t bwd_reduce_t(const BnBwdArgs& a, hipStream_t s) {
   if (a.mask && !bwd_v8<T, TZ>(a)) return hipErrorInvalidValue;   // bits exist on the 8-wide path only
   const bool rdh = a.reduce_dyhat && a.dyhat;
   if ((a.dshift || rdh) && (!a.mask || a.dzscale || !bwd_v8<T, TZ>(a))) return hipErrorInvalidValue;
+  if (a.cs_part && (!a.dshift || rdh || !a.beta || sizeof(T) != 2)) return hipErrorInvalidValue;
   if (bwd_v8<T, TZ>(a)) {
     const int cg_n = a.C / 8;
     const dim3 g(a.rb, cg_n > 256 ? ceil_div(cg_n, 256) : 1);
-    if (a.mask && a.dshift && rdh) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 2, 1>), g, dim3(256), 0, s, a);
+    if (a.cs_part) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 2, 0, 1>), g, dim3(256), 0, s, a);
+    else if (a.mask && a.dshift && rdh) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 2, 1>), g, dim3(256), 0, s, a);
     else if (a.mask && a.dshift) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 2, 0>), g, dim3(256), 0, s, a);
     else if (a.mask && rdh) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 0, 1>), g, dim3(256), 0, s, a);
     else if (a.mask) hipLaunchKernelGGL((bn_bwd_reduce8_kernel<T, TZ, 2, 0>), g, dim3(256), 0, s, a);

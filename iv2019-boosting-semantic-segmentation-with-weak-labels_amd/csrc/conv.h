@@ -107,8 +107,9 @@ hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s);
 // epilogue of one tile inside the next tile's main loop; BN partials per 64 rows
 bool conv_nt_db_ok(const ConvArgs& a);
 hipError_t launch_conv_nt_db(int dtype, const ConvArgs& a, hipStream_t s);
-// launches that apply ConvArgs::omask: 16-bit dense 1x1 ping-pong with a residual (one tile per
-// workgroup), i.e. the identity units' conv1 data gradient
+// launches that apply ConvArgs::omask: 16-bit dense 1x1 ping-pong, one tile per workgroup (the
+// identity units' conv1 data gradient with its residual; a projection unit's K-concatenated
+// conv1 + shortcut data gradient; decrease_fdims' data gradient into block4)
 bool conv_nt_omask_ok(int dtype, const ConvArgs& a);
 // launches that can fold the BN-backward reduce (ConvArgs::bq_*) into the epilogue
 bool conv_nt_bq_ok(int dtype, const ConvArgs& a);

@@ -778,7 +778,7 @@ hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
     if constexpr (ST == 0 || ST == 1) return pp_launch<E, ST, 2>(a, s);
     return hipErrorInvalidValue;
   }
-  if (a.r || a.r2) return pp_launch<E, ST, 0>(a, s);
+  if (a.r || a.r2 || a.omask) return pp_launch<E, ST, 0>(a, s);
   return pp_launch<E, ST, 1>(a, s);
 }
 
@@ -805,8 +805,8 @@ bool conv_nt_bq_ok(int dtype, const ConvArgs& a) {
 
 bool conv_nt_omask_ok(int dtype, const ConvArgs& a) {
   return seg_half(dtype) && !a.tap8 && a.st == 1 && a.KH == 1 && a.KW == 1 && a.sf == 1 &&
-         a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho && a.W == a.Wo && !a.x2 && (a.r || a.r2) &&
-         a.Co > 128 && conv_nt_pp_ok(a) && a.ldm >= a.Co / 8;
+         a.pad_h == 0 && a.pad_w == 0 && a.H == a.Ho && a.W == a.Wo && a.Co > 128 &&
+         conv_nt_pp_ok(a) && a.ldm >= a.Co / 8;
 }
 
 template <typename E>

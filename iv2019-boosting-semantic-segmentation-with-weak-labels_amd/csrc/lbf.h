@@ -33,7 +33,8 @@ struct LbfCombineArgs {
   const void* w;        // W3, 16-bit [co][ci]
   const float* g;       // [ci][ci] Gram matrix y2^T y2
   const float* p1;      // [co][ci] dyhat^T y2
-  const float* cspart;  // [rb][ci] column-sum partials of y2
+  const float* cspart;  // [rb][ci] column-sum partials of y2 (the unit's conv2 BN-backward reduce,
+                        // BnBwdArgs::cs_part)
   int rb;
   const float* coef;    // [3][co] = A, B, D
   float* out;           // [co][ci] weight gradient (fp32)
@@ -44,7 +45,4 @@ hipError_t launch_lbf_prep(int dtype, const LbfPrepArgs& a, hipStream_t s);
 // the co / 128 chunk partials of the prep (fixed order)
 hipError_t launch_lbf_hreduce(int dtype, const float* slab, int splits, long n, void* h,
                               const float* bpart, int nbp, int ci, float* bias, hipStream_t s);
-// per row block column sums of a 16-bit [M][ld] activation's first C channels (C % 8 == 0, C <= 2048)
-hipError_t launch_lbf_colsum(int dtype, const void* y, long M, int C, int ld, float* part, int rb,
-                             hipStream_t s);
 hipError_t launch_lbf_combine(int dtype, const LbfCombineArgs& a, hipStream_t s);

@@ -103,52 +103,6 @@ __global__ __launch_bounds__(256) void lbf_hreduce_kernel(const float* __restric
   }
 }
 
-// block b sums rows [b * rows_per, ...) of every channel: threads = 8-channel groups x row
-// lanes, four rows in flight per lane, row lanes combined through LDS in order
-template <typename T>
-__global__ __launch_bounds__(256) void lbf_colsum_kernel(const T* __restrict__ y, long M, int C, int ld,
-                                                         float* __restrict__ part, int rb) {
-  __shared__ float sh[256 * 8];
-  const int cgn = C / 8;                 // <= 256 (host)
-  const int rpp = 256 / cgn;
-  const int cg = threadIdx.x % cgn, rl = threadIdx.x / cgn;
-  const long rows_per = (M + rb - 1) / rb;
-  const long r0 = (long)blockIdx.x * rows_per;
-  const long r1 = r0 + rows_per < M ? r0 + rows_per : M;
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (rl < rpp) {
-    long m = r0 + rl;
-    for (; m + 7L * rpp < r1; m += 8L * rpp) {
-      uint4 raw[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) raw[u] = *(const uint4*)(y + (size_t)(m + (long)u * rpp) * ld + cg * 8);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        float v[8];
-        Half<T>::unpack(raw[u], v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) s[e] += v[e];
-      }
-    }
-    for (; m < r1; m += rpp) {
-      float v[8];
-      Vec8<T>::load(y + (size_t)m * ld + cg * 8, v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += v[e];
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) sh[threadIdx.x * 8 + e] = s[e];
-  __syncthreads();
-  if (rl == 0) {
-    for (int r = 1; r < rpp; ++r)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += sh[(r * cgn + cg) * 8 + e];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) part[(size_t)blockIdx.x * C + cg * 8 + e] = s[e];
-  }
-}
-
 // out[c][k] = A_c p1[c][k] + B_c colsum_k + D_c (W3 G)[c][k]: a 32 x 64 output tile per block,
 // 2 x 4 per thread, the W3 G product in fp32 through LDS in 32-deep chunks, the next chunk's
 // global loads issued before the current chunk's FMAs
@@ -272,18 +226,6 @@ hipError_t launch_lbf_hreduce(int dtype, const float* slab, int splits, long n, 
   else if (dtype == SEG_BF16)
     hipLaunchKernelGGL(lbf_hreduce_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, slab, splits, n, (bf16_t*)h,
                        bpart, nbp, ci, bias);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-hipError_t launch_lbf_colsum(int dtype, const void* y, long M, int C, int ld, float* part, int rb,
-                             hipStream_t s) {
-  if (C % 8 || C > 2048 || ld % 8 || 256 % (C / 8)) return hipErrorInvalidValue;
-  if (dtype == SEG_F16)
-    hipLaunchKernelGGL(lbf_colsum_kernel<f16_t>, dim3(rb), dim3(256), 0, s, (const f16_t*)y, M, C, ld, part, rb);
-  else if (dtype == SEG_BF16)
-    hipLaunchKernelGGL(lbf_colsum_kernel<bf16_t>, dim3(rb), dim3(256), 0, s, (const bf16_t*)y, M, C, ld, part, rb);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

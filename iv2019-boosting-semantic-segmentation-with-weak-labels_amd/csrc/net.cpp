@@ -70,6 +70,7 @@ struct ConvL {
   // [3][co] of the last backward, the gated gradient it read (seg_debug_tensor materialises dy
   // from it on request: the step itself never writes dy of such a layer)
   float* lbf_coef = nullptr;
+  float* lbf_cs = nullptr;        // [rb of the unit's conv2 BN][ci] column-sum partials of y2
   bool lbf_done = false;          // folded in the last backward
   bool lbf_dy_ready = false;      // ... and dy materialised since (seg_debug_tensor)
   Act lbf_dyhat;
@@ -249,7 +250,6 @@ struct seg_ctx {
   float* lbf_bias = nullptr;
   float* lbf_bpart = nullptr;
   float* lbf_p1 = nullptr;
-  float* lbf_cs = nullptr;
   int64_t lbf_launches = 0;        // layers folded (seg_counter)
   bool bq_on = false;              // SEG_BN_FOLD=1 at creation: BN-backward reduce folded (A/B; -1.3 %)
   bool defer_red = false;          // this step's non-stem reduces are deferred
@@ -652,7 +652,7 @@ int gn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
 // gradient stored by the reduce when dyhat_out is given
 int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const Act* dyhat_out,
                 const float* dzscale = nullptr, const float* dshift = nullptr,
-                bool reduce_only = false) {
+                bool reduce_only = false, float* cs_out = nullptr) {
   seg_ctx* c = S.c;
   if (c->gn) return gn_backward(S, li, dz, dz_f32, z, dyhat_out, dzscale);
   ConvL& L = c->convs[li];
@@ -669,7 +669,8 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   a.dzscale = dzscale;
   a.dshift = dshift;
   a.reduce_dyhat = reduce_only && dyhat_out ? 1 : 0;
-  if ((dshift || a.reduce_dyhat) && !a.mask)
+  if (cs_out) { a.cs_part = cs_out; a.beta = c->params + L.b_off; }
+  if ((dshift || a.reduce_dyhat || cs_out) && !a.mask)
     return set_err(&c->err, -EINVAL, "bn_backward %s: shift / reduce-side dyhat need the ReLU bits", L.name.c_str());
   const double esz = seg_half(S.dt) ? 2.0 : 4.0, zsz = dz_f32 ? 4.0 : esz;
   const double me = a.M * (double)a.C * 1e-9;
@@ -831,8 +832,10 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
 
 // dx = dgrad(li) + dgrad(li2) in one K-concatenated ping-pong launch: a projection unit's conv1
 // and shortcut (both 1 x 1, stride 1, the unit input's geometry). Returns 1 when the shapes do
-// not fit that path (the caller then runs the two data gradients with the residual add)
-int conv_dgrad_dual(Step& S, int li, int li2, const Act& dx) {
+// not fit that path (the caller then runs the two data gradients with the residual add).
+// omask (in / out): ReLU bits to store dx masked by (premask_bits), reset to nullptr when the
+// launch cannot take them
+int conv_dgrad_dual(Step& S, int li, int li2, const Act& dx, const uint8_t** omask = nullptr) {
   seg_ctx* c = S.c;
   const ConvL& L = c->convs[li];
   const ConvL& L2 = c->convs[li2];
@@ -844,6 +847,10 @@ int conv_dgrad_dual(Step& S, int li, int li2, const Act& dx) {
   a.x2 = L2.dy.p; a.ldx2 = L2.dy.ld; a.C2 = L2.co;
   a.w2 = L2.wt_lp; a.ldw2 = L2.co;
   if (a.st != 1 || a.sf != 1 || a.pad_h || a.pad_w || !conv_nt_pp_ok(a)) return 1;
+  if (omask && *omask) {   // stored masked by the consumer's ReLU bits where that launch exists
+    a.omask = *omask; a.ldm = a.Co / 8;
+    if (!conv_nt_omask_ok(S.dt, a)) { a.omask = nullptr; *omask = nullptr; }
+  }
   const long M = (long)L.N * L.H * L.W;
   const double gbx = ((double)M * (L.co + L2.co) + (double)(L.co + L2.co) * L.ci + (double)M * L.ci) *
                      c->esz * 1e-9;
@@ -1016,20 +1023,16 @@ int make_resize_grid(seg_ctx* c, GridSpec& g, int kr, int kc, int H, int W) {
 // graph construction + allocation
 // ------------------------------------------------------------------------------------------
 // linear BN-backward fold (lbf.h): the unit shapes it applies to -- a 16-bit batch-norm
-// identity unit whose conv3 is an expansion 1 x 1 (co >= 2 ci, ci a multiple of 64; its data
+// identity or subsample unit whose conv3 is an expansion 1 x 1 (co >= 2 ci, ci a multiple of 64; its data
 // gradient is a ping-pong launch for ci > 128, a v2 launch otherwise: C2 = ci, Co = ci) and whose
 // conv2 output gate is kept as bits
-constexpr int LBF_RB = 256;   // row blocks of the conv input's column sums
-#ifndef LBF_MIN_CI
-#define LBF_MIN_CI 64   // A/B builds: 256 = block3-4 only (the first version)
-#endif
 int lbf_hsplits(const ConvL& L3) { return std::max(1, L3.co / 128); }   // H: 128 channels per split
 
 bool lbf_shape_ok(const seg_ctx* c, const Unit& u) {
-  if (!seg_half(c->dt) || c->gn || u.kind != SC_IDENTITY || u.c3 < 0 || u.c2 < 0) return false;
+  if (!seg_half(c->dt) || c->gn || u.kind == SC_CONV || u.c3 < 0 || u.c2 < 0) return false;
   const ConvL& L3 = c->convs[u.c3];
   const ConvL& L2 = c->convs[u.c2];
-  return L3.k == 1 && L3.stride == 1 && L3.rate == 1 && L3.co >= 2 * L3.ci && L3.ci >= LBF_MIN_CI &&
+  return L3.k == 1 && L3.stride == 1 && L3.rate == 1 && L3.co >= 2 * L3.ci && L3.ci >= 64 &&
          L3.co <= 2048 && L3.ci % 64 == 0 && L3.co % 128 == 0 && L2.co == L3.ci && L2.relu;
 }
 
@@ -1361,6 +1364,9 @@ int build(seg_ctx* c) {
       if (!lbf_shape_ok(c, u)) continue;
       ConvL& L3 = c->convs[u.c3];
       if (int r = dalloc(c, &L3.lbf_coef, 3 * (size_t)L3.co)) return r;
+      // per layer: conv2's BN reduce writes it on the compute stream while the side stream may
+      // still be combining an earlier unit's gradient
+      if (int r = dalloc(c, &L3.lbf_cs, (size_t)c->convs[u.c2].rb * L3.ci)) return r;
       wts = std::max(wts, (size_t)L3.co * L3.ci);
       hh = std::max(hh, (size_t)L3.ci * L3.ci);
       hs = std::max(hs, (size_t)lbf_hsplits(L3) * L3.ci * L3.ci);
@@ -1378,7 +1384,6 @@ int build(seg_ctx* c) {
       if (int r = dalloc(c, &c->lbf_bias, ci_max)) return r;
       if (int r = dalloc(c, &c->lbf_bpart, (wts / 128) + ci_max)) return r;   // [co / 128][ci]
       if (int r = dalloc(c, &c->lbf_p1, wts + hh)) return r;   // [P1 (co x ci) | G (ci x ci)]
-      if (int r = dalloc(c, &c->lbf_cs, (size_t)LBF_RB * ci_max)) return r;
     }
   }
   return 0;
@@ -1414,6 +1419,17 @@ bool premask_ok(seg_ctx* c, const Unit& u, const Unit* pred, bool accumulate) {
   ConvArgs a = dgrad_args(c, u.c1, pred->dout, &u.dpre, nullptr);
   a.ldm = a.Co / 8;
   return conv_nt_omask_ok(c->dt, a);
+}
+
+// the ReLU bits of pred's output when the data gradient into it (of C channels) may be stored
+// masked by them: pred an identity or subsample unit, so its c3 BN backward then reads dout
+// ungated and writes no dpre (block boundaries: a projection unit's dual data gradient,
+// decrease_fdims')
+const uint8_t* premask_bits(seg_ctx* c, const Unit* pred, int C) {
+  if (!c->premask || !pred || pred->kind == SC_CONV || c->gn || !pred->out.mask ||
+      pred->out.C != C || c->convs[pred->c3].co != C)
+    return nullptr;
+  return pred->out.mask;
 }
 
 // ---- linear BN-backward fold of an identity unit's conv3 (lbf.h) ----
@@ -1483,10 +1499,29 @@ int lbf_wgrad(Step& S, Unit& u, const Act& dyhat) {
     HIPCALL(c, launch_conv_wgrad_pp(S.dt, a, W.s));
     HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, n1, n1, c->lbf_p1, 0, W.s));
   }
-  HIPCALL(c, launch_lbf_colsum(S.dt, y2.p, y2.M(), y2.C, y2.ld, c->lbf_cs, LBF_RB, W.s));
+  return prof_end(c, W.s, slot);
+}
+
+// dW3 = A o P1 + B (x) colsum + D o (W3 G) into the gradient buffer, after the unit's conv2
+// BN-backward reduce has written the column sums of y2 (recomputed there from z2 exactly as
+// the forward BN apply formed y2: a separate pass over y2 measured the same step time,
+// profiles/r05_s26_premask_cs_wg_ab.txt), on the weight-gradient stream when it is active
+int lbf_combine(Step& S, Unit& u) {
+  seg_ctx* c = S.c;
+  const int li = u.c3;
+  ConvL& L = c->convs[li];
+  Step W = S;
+  if (c->side_active) {
+    HIPCALL(c, hipEventRecord(c->ev_dy[li], S.s));
+    HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_dy[li], 0));
+    W.s = c->side;
+  }
+  int slot;
+  if (int r = prof_begin(c, W.s, 2, li, 0.0, &slot, 0.0)) return r;
   LbfCombineArgs cb{};
   cb.co = L.co; cb.ci = L.ci; cb.w = L.w_lp; cb.g = c->lbf_p1 + (size_t)L.co * L.ci; cb.p1 = c->lbf_p1;
-  cb.cspart = c->lbf_cs; cb.rb = LBF_RB; cb.coef = L.lbf_coef; cb.out = c->grads + L.w_off;
+  cb.cspart = L.lbf_cs; cb.rb = c->convs[u.c2].rb;
+  cb.coef = L.lbf_coef; cb.out = c->grads + L.w_off;
   HIPCALL(c, launch_lbf_combine(S.dt, cb, W.s));
   if (int r = prof_end(c, W.s, slot)) return r;
   c->wg_done[li] = 1;
@@ -1577,7 +1612,11 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred =
     if (int r = conv_wgrad(S, u.c3, u.z2)) return r;
     if (int r = conv_dgrad(S, u.c3, u.dz2, nullptr, nullptr, nullptr, u.c2, &u.z2)) return r;
   }
-  if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr, nullptr, lbf ? c->lbf_bias : nullptr)) return r;
+  if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr, nullptr, lbf ? c->lbf_bias : nullptr, false,
+                         lbf ? L3.lbf_cs : nullptr))
+    return r;
+  if (lbf)
+    if (int r = lbf_combine(S, u)) return r;
   if (int r = conv_wgrad(S, u.c2, u.z1)) return r;
   if (int r = conv_dgrad(S, u.c2, u.dz1, nullptr, nullptr, nullptr, u.c1, &u.z1)) return r;
   if (int r = bn_backward(S, u.c1, u.dz1, 0, &u.z1, nullptr)) return r;
@@ -1602,7 +1641,12 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred =
     case SC_CONV: {
       if (int r = conv_wgrad(S, u.sc, u.in)) return r;
       if (!accumulate) {   // one K-concatenated GEMM when both are 1 x 1 stride-1 ping-pong shapes
-        const int r = conv_dgrad_dual(S, u.c1, u.sc, dx);
+        const uint8_t* pm = premask_bits(c, pred, c->convs[u.c1].ci);
+        const int r = conv_dgrad_dual(S, u.c1, u.sc, dx, &pm);
+        if (r == 0 && pm) {
+          pred->dout_masked = true;   // only once the masked store is enqueued
+          ++c->premask_launches;
+        }
         if (r <= 0) return r;
       }
       if (int r = conv_dgrad(S, u.c1, dx, accumulate ? &dx : nullptr)) return r;
@@ -1837,7 +1881,17 @@ int backward_layers(Step& S) {
     return r;
   }
   if (int r = conv_wgrad(S, c->dfd, c->units.back().out)) return r;
-  if (int r = conv_dgrad(S, c->dfd, c->units.back().dout)) return r;
+  {
+    Unit& last = c->units.back();
+    const uint8_t* pm = premask_bits(c, &last, c->convs[c->dfd].ci);
+    if (pm) {
+      ConvArgs a = dgrad_args(c, c->dfd, last.dout, nullptr, nullptr);
+      a.omask = pm; a.ldm = a.Co / 8;
+      if (!conv_nt_omask_ok(S.dt, a)) pm = nullptr;
+    }
+    if (int r = conv_dgrad(S, c->dfd, last.dout, nullptr, nullptr, pm)) return r;
+    if (pm) { last.dout_masked = true; ++c->premask_launches; }
+  }
   for (int i = (int)c->units.size() - 1; i >= 0; --i) {
     const Act& dx = i == 0 ? c->dp0 : c->units[i - 1].dout;
     if (int r = unit_backward(S, c->units[i], dx, false, i == 0 ? nullptr : &c->units[i - 1])) return r;

@@ -353,8 +353,8 @@ def test_bn_fold_matches(cuda, monkeypatch):
 
 def test_lbf_matches(cuda, monkeypatch):
     """Linear BN-backward fold (round 5, csrc/lbf.h): the conv3 BN-backward apply of the 16-bit
-    identity units with an expanding conv3 (block1 unit 2 -- unit 3 subsamples --, block2 units
-    2-4, block3 units 2-6, block4 units 2-3 of R50 at OS 8; block1-2 data gradients on the v2
+    identity and subsample units with an expanding conv3 (block1 units 2-3, block2 units 2-4,
+    block3 units 2-6, block4 units 2-3 of R50 at OS 8; block1-2 data gradients on the v2
     kernel's K-concatenated path) is
     replaced by the affine form dz3 = A dyhat + B + D z3 pushed through the data gradient
     ([dyhat | y2] x [A o W3 ; W3^T diag(D) W3], constant added by conv2's BN backward) and the
@@ -384,7 +384,7 @@ def test_lbf_matches(cuda, monkeypatch):
         torch.cuda.synchronize()
         out.append((ctx.outputs()[0].cpu().numpy().copy(), ctx.named("grads")))
         n = ctx.counter("lbf_layers")
-        assert n == (1 + 3 + 5 + 2 if on == "1" else 0), (on, n)
+        assert n == (2 + 3 + 5 + 2 if on == "1" else 0), (on, n)
         ctx.close()
     (l0, g0), (l1, g1) = out
     assert np.array_equal(l0, l1)
