@@ -709,7 +709,9 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
 // shortcut BN): one dual reduce and one dual apply read dz and the bits once for both; each
 // layer keeps its own finalize. Batch norm, 16-bit or fp32 dz of the storage type, no
 // cross-replica exchange (that path runs the two layers through bn_backward)
-int bn_backward_dual(Step& S, int li, int li2, const Act& dz, const Act& z) {
+// second_only: dz arrived pre-masked and the first layer's apply is folded (lbf.h): after the
+// dual reduce and both finalizes only the second layer's apply runs (ungated)
+int bn_backward_dual(Step& S, int li, int li2, const Act& dz, const Act& z, bool second_only = false) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
   ConvL& L2 = c->convs[li2];
@@ -738,6 +740,17 @@ int bn_backward_dual(Step& S, int li, int li2, const Act& dz, const Act& z) {
   HIPCALL(c, launch_bn_bwd_finalize(L2.bwd_part, L2.rb, a.M, L2.co, L2.st,
                                     tb ? c->grads + L2.g_off : nullptr,
                                     tb ? c->grads + L2.b_off : nullptr, S.s, c->bn_infer));
+  if (second_only) {
+    BnBwdArgs b{};
+    b.dz = dz.p; b.lddz = dz.ld;
+    b.y = L2.y.p; b.ldy = L2.y.ld; b.M = a.M; b.C = L2.co;
+    b.mean = L2.st.mean; b.invstd = L2.st.invstd; b.scale = L2.st.scale;
+    b.sdy = L2.st.sdy; b.sdyx = L2.st.sdyx;
+    b.dy = L2.dy.p; b.lddy = L2.dy.ld;
+    if (int r = prof_begin(c, S.s, 5, li2, me * 3 * esz, &slot)) return r;
+    HIPCALL(c, launch_bn_bwd_apply(S.dt, 0, b, S.s));
+    return prof_end(c, S.s, slot);
+  }
   if (int r = prof_begin(c, S.s, 5, li, gb_in + me * 2 * esz, &slot)) return r;
   HIPCALL(c, launch_bn_bwd_apply_dual(S.dt, a, S.s));
   return prof_end(c, S.s, slot);
@@ -1023,13 +1036,13 @@ int make_resize_grid(seg_ctx* c, GridSpec& g, int kr, int kc, int H, int W) {
 // graph construction + allocation
 // ------------------------------------------------------------------------------------------
 // linear BN-backward fold (lbf.h): the unit shapes it applies to -- a 16-bit batch-norm
-// identity or subsample unit whose conv3 is an expansion 1 x 1 (co >= 2 ci, ci a multiple of 64; its data
+// bottleneck (identity, subsample, or projection with its output gradient pre-masked) whose conv3 is an expansion 1 x 1 (co >= 2 ci, ci a multiple of 64; its data
 // gradient is a ping-pong launch for ci > 128, a v2 launch otherwise: C2 = ci, Co = ci) and whose
 // conv2 output gate is kept as bits
 int lbf_hsplits(const ConvL& L3) { return std::max(1, L3.co / 128); }   // H: 128 channels per split
 
 bool lbf_shape_ok(const seg_ctx* c, const Unit& u) {
-  if (!seg_half(c->dt) || c->gn || u.kind == SC_CONV || u.c3 < 0 || u.c2 < 0) return false;
+  if (!seg_half(c->dt) || c->gn || u.c3 < 0 || u.c2 < 0) return false;
   const ConvL& L3 = c->convs[u.c3];
   const ConvL& L2 = c->convs[u.c2];
   return L3.k == 1 && L3.stride == 1 && L3.rate == 1 && L3.co >= 2 * L3.ci && L3.ci >= 64 &&
@@ -1413,7 +1426,7 @@ int unit_forward(Step& S, Unit& u) {
 // pred's dpre, pred's own conv1 residual), so pred's c3 BN backward neither reads the bits nor
 // writes dpre (one M x C store pass fewer per such unit)
 bool premask_ok(seg_ctx* c, const Unit& u, const Unit* pred, bool accumulate) {
-  if (!c->premask || !pred || accumulate || u.kind != SC_IDENTITY || pred->kind != SC_IDENTITY || c->gn)
+  if (!c->premask || !pred || accumulate || u.kind != SC_IDENTITY || pred->kind == SC_SUBSAMPLE || c->gn)
     return false;
   if (!pred->out.mask || pred->out.C != c->convs[u.c1].ci || c->convs[pred->c3].co != pred->out.C) return false;
   ConvArgs a = dgrad_args(c, u.c1, pred->dout, &u.dpre, nullptr);
@@ -1433,8 +1446,15 @@ const uint8_t* premask_bits(seg_ctx* c, const Unit* pred, int C) {
 }
 
 // ---- linear BN-backward fold of an identity unit's conv3 (lbf.h) ----
-bool lbf_ok(seg_ctx* c, const Unit& u) {
+// in_masked: u.dout arrived pre-masked (a projection unit folds only then: its gated gradient
+// is dout itself, and its dual BN reduce cannot store one)
+bool lbf_ok(seg_ctx* c, const Unit& u, bool in_masked) {
   if (!c->lbf_on || c->bq_on || !c->lbf_wts || !lbf_shape_ok(c, u)) return false;
+  if (u.kind == SC_CONV) {
+    const ConvL& L3 = c->convs[u.c3];
+    const ConvL& Ls = c->convs[u.sc];
+    if (!in_masked || c->sync_fn || Ls.co != L3.co || Ls.rb != L3.rb || Ls.y.M() != L3.y.M()) return false;
+  }
   const ConvL& L3 = c->convs[u.c3];
   if (!L3.lbf_coef || !L3.wt_lp || !u.out.mask || u.out.C != L3.co || !u.z2.mask ||
       u.z2.C != L3.ci || u.dz2.C != L3.ci)
@@ -1445,7 +1465,7 @@ bool lbf_ok(seg_ctx* c, const Unit& u) {
   a.y = u.dz2.p; a.Ho = L3.H; a.Wo = L3.W; a.Co = L3.ci; a.ldy = u.dz2.ld;
   a.x2 = u.z2.p; a.ldx2 = u.z2.ld; a.C2 = L3.ci; a.w2 = c->lbf_h; a.ldw2 = L3.ci;
   a.KH = a.KW = 1; a.sf = 1; a.st = 1; a.dil = 1;
-  if (u.dpre.ld != u.dout.ld) return false;
+  if (u.kind != SC_CONV && u.dpre.ld != u.dout.ld) return false;
   return L3.ci > 128 ? conv_nt_pp_ok(a) : conv_nt_v2_ok(a) && conv_nt_v2_dual_ok(a);
 }
 
@@ -1593,13 +1613,18 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred =
   const Act& dres = in_masked ? u.dout : u.dpre;   // the masked dout, wherever it lives
   const ConvL& L3 = c->convs[u.c3];
   const ConvL& Ls = c->convs[u.kind == SC_CONV ? u.sc : u.c3];
-  const bool lbf = lbf_ok(c, u);
+  const bool lbf = lbf_ok(c, u, in_masked);
   if (lbf) {
     // linear BN-backward fold: reduce + finalize of conv3's BN (the gated gradient into dpre
-    // by the reduce itself when dout is not pre-masked), then no apply pass (lbf_backward)
-    if (int r = bn_backward(S, u.c3, u.dout, 0, in_masked ? nullptr : &u.out, dpre, nullptr, nullptr, true))
+    // by the reduce itself when dout is not pre-masked; a projection unit's dual reduce, then
+    // the shortcut BN's apply alone), then no conv3 apply pass (lbf_backward)
+    if (u.kind == SC_CONV) {
+      if (int r = bn_backward_dual(S, u.c3, u.sc, u.dout, u.out, true)) return r;
+    } else if (int r = bn_backward(S, u.c3, u.dout, 0, in_masked ? nullptr : &u.out, dpre, nullptr, nullptr,
+                                   true)) {
       return r;
-    if (int r = lbf_backward(S, u, dres)) return r;
+    }
+    if (int r = lbf_backward(S, u, u.kind == SC_CONV ? u.dout : dres)) return r;
   } else {
     if (u.kind == SC_CONV && !c->gn && !c->sync_fn && u.out.mask && u.out.C == L3.co &&
         Ls.co == L3.co && Ls.rb == L3.rb && Ls.y.M() == L3.y.M()) {

@@ -255,11 +255,15 @@ def test_defer_stem_update_matches(cuda, monkeypatch, dtype, defer_reduce):
 
 
 @pytest.mark.parametrize("dtype,depth", [("bf16", 50), ("fp16", 101)])
-def test_premask_matches(cuda, dtype, depth):
-    """seg_set_premask (identity units' conv1 data gradient stores the previous unit's output
-    gradient already ReLU-masked; that unit's c3 BN backward then reads it without the bits and
-    writes no separate masked copy): three steps give bitwise the same losses, gradients,
-    parameters and momentum as the path that masks in the BN backward."""
+def test_premask_matches(cuda, dtype, depth, monkeypatch):
+    """seg_set_premask (identity units' conv1 data gradient, a projection unit's dual data
+    gradient and decrease_fdims' store the previous unit's output gradient already ReLU-masked;
+    that unit's c3 BN backward then reads it without the bits and writes no separate masked
+    copy): three steps give bitwise the same losses, gradients, parameters and momentum as the
+    path that masks in the BN backward. With the linear BN-backward fold off (SEG_LBF=0): a
+    projection unit folds only when its gradient arrives pre-masked, so with the fold on the
+    two arms would differ by the fold's own rounding (test_lbf_matches covers that)."""
+    monkeypatch.setenv("SEG_LBF", "0")
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     cfg = SegConfig(depth=depth, height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp")
@@ -353,9 +357,9 @@ def test_bn_fold_matches(cuda, monkeypatch):
 
 def test_lbf_matches(cuda, monkeypatch):
     """Linear BN-backward fold (round 5, csrc/lbf.h): the conv3 BN-backward apply of the 16-bit
-    identity and subsample units with an expanding conv3 (block1 units 2-3, block2 units 2-4,
-    block3 units 2-6, block4 units 2-3 of R50 at OS 8; block1-2 data gradients on the v2
-    kernel's K-concatenated path) is
+    bottlenecks with an expanding conv3 (every unit of R50's four blocks: the projection units
+    through their pre-masked output gradient, their shortcut BN applied alone after the dual
+    reduce; block1-2 data gradients on the v2 kernel's K-concatenated path) is
     replaced by the affine form dz3 = A dyhat + B + D z3 pushed through the data gradient
     ([dyhat | y2] x [A o W3 ; W3^T diag(D) W3], constant added by conv2's BN backward) and the
     weight gradient (A o dyhat^T y2 + B colsum(y2) + D o W3 y2^T y2). Against SEG_LBF=0 on the
@@ -384,7 +388,7 @@ def test_lbf_matches(cuda, monkeypatch):
         torch.cuda.synchronize()
         out.append((ctx.outputs()[0].cpu().numpy().copy(), ctx.named("grads")))
         n = ctx.counter("lbf_layers")
-        assert n == (2 + 3 + 5 + 2 if on == "1" else 0), (on, n)
+        assert n == (3 + 4 + 6 + 3 if on == "1" else 0), (on, n)
         ctx.close()
     (l0, g0), (l1, g1) = out
     assert np.array_equal(l0, l1)
