@@ -479,6 +479,9 @@ def main():
         # the north star's named target: the dilated 3x3 convs of the encoder (block3 rate 2,
         # block4 rate 4, and the ASPP rates), per pass, against the MFMA peak
         dump = ctx.profile_dump()
+        if os.environ.get("SEG_BENCH_DUMP"):   # diagnostics: the profiled step's records
+            with open(os.environ["SEG_BENCH_DUMP"], "w") as f:
+                json.dump(dump, f)
         # compulsory HBM bytes per launch of the dominant class (every operand once; for the
         # weight gradient x + dy in 16 bit and the fp32 dW): traffic / this = re-read factor
         rows_dom = [row for row in dump if row["cls"] == dom]
