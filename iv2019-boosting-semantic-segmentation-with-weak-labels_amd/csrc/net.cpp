@@ -1486,8 +1486,8 @@ int lbf_wgrad(Step& S, Unit& u, const Act& dyhat) {
   const long P = (long)L.N * L.Ho * L.Wo;
   const long n1 = (long)(L.co + L.ci) * L.ci;
   int slot;
-  // algorithmic work of the layer's weight gradient; the G rows, the column sums and the
-  // combine are time of this class too
+  // algorithmic work of the layer's weight gradient; the G rows are time of this class too
+  // (the combine is recorded with the BN-backward apply class, lbf_combine)
   const double gbx = (((double)P * L.co + (double)P * L.ci) * c->esz + (double)L.co * L.ci * 4.0) * 1e-9;
   if (int r = prof_begin(c, W.s, 2, li, 2.0 * P * L.co * L.ci * 1e-9, &slot, gbx)) return r;
   if (L.ci < 256) {   // narrow ci: P1 and G as two weight-gradient launches of their own tile shapes
@@ -1537,7 +1537,11 @@ int lbf_combine(Step& S, Unit& u) {
     W.s = c->side;
   }
   int slot;
-  if (int r = prof_begin(c, W.s, 2, li, 0.0, &slot, 0.0)) return r;
+  // profiled as BN-backward apply time with the prep and H (the B and D terms it adds are that
+  // pass's affine part); its bytes: P1, G, W3, the column-sum partials and the result
+  const double gbc = ((double)L.co * L.ci * (4.0 + c->esz + 4.0) + (double)L.ci * L.ci * 4.0 +
+                      (double)c->convs[u.c2].rb * L.ci * 4.0) * 1e-9;
+  if (int r = prof_begin(c, W.s, 5, li, gbc, &slot)) return r;
   LbfCombineArgs cb{};
   cb.co = L.co; cb.ci = L.ci; cb.w = L.w_lp; cb.g = c->lbf_p1 + (size_t)L.co * L.ci; cb.p1 = c->lbf_p1;
   cb.cspart = L.lbf_cs; cb.rb = c->convs[u.c2].rb;
