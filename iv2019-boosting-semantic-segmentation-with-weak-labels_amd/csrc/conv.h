@@ -61,9 +61,9 @@ struct WgradArgs {
   int KH, KW, sf, pad_h, pad_w, dil;
   float* out;      // fp32 [splits][Co][KH*KW*C]
   int splits;
-  // optional second dy source (256 x 256 ping-pong kernel only): rows co >= Co1 of the output
-  // take dy2 [P][lddy2] column co - Co1 (Co1 % 256 == 0): two weight-gradient GEMMs over the
-  // same x in one launch (csrc/lbf.h: dyhat^T y2 and y2^T y2)
+  // optional second dy source (16-bit v2 / ping-pong kernels): rows co >= Co1 of the output
+  // take dy2 [P][lddy2] column co - Co1 (Co1 % 8 == 0; the ping-pong kernel Co1 % 256 == 0):
+  // two weight-gradient GEMMs over the same x in one launch (csrc/lbf.h: dyhat^T y2, y2^T y2)
   const void* dy2;
   int lddy2, Co1;
 };

@@ -822,6 +822,7 @@ hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t
 }
 
 hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s) {
+  if (a.dy2 && !(seg_half(dtype) && a.KH == 1 && a.KW == 1 && conv_wgrad_v2_ok(a))) return hipErrorInvalidValue;
   if (seg_half(dtype) && conv_wgrad_patch_ok(a)) return launch_conv_wgrad_patch(dtype, a, s);
   if (seg_half(dtype) && conv_wgrad_v2_ok(a)) return launch_conv_wgrad_v2(dtype, a, s);
   if (dtype == SEG_BF16) return wg_dispatch<bf16_t>(a, s);

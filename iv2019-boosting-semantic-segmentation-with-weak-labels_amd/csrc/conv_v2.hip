@@ -1015,11 +1015,18 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
   const E* zero = (const E*)g_zero16;
 
   // ---- launch-invariant per-lane decode ----
-  int a_row[AI], a_co[AI];
+  // a lane's 8 output rows come from dy, or from dy2 at rows >= Co1 (WgradArgs::dy2; Co1 % 8
+  // == 0, so a 16-B chunk never straddles the two)
+  int a_row[AI], a_co[AI], a_col[AI], a_ld[AI];
+  const E* a_src[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     a_row[i] = (i * 8 + wave) * RPI_A + lane / CPR_A;
     a_co[i] = m0 + wswz<BM>(a_row[i], lane % CPR_A) * 8;
+    const bool sec = a.dy2 && a_co[i] >= a.Co1;
+    a_src[i] = sec ? (const E*)a.dy2 : DY;
+    a_col[i] = sec ? a_co[i] - a.Co1 : a_co[i];
+    a_ld[i] = sec ? a.lddy2 : a.lddy;
   }
   int b_row[BI], b_dh[BI], b_dw[BI], b_ci[BI];
   bool b_ok[BI];
@@ -1044,7 +1051,7 @@ __global__ __launch_bounds__(WG_THREADS, 1) void conv_wgrad_v2_kernel(WgradArgs 
     for (int i = 0; i < AI; ++i) {
       const int p = p0 + a_row[i];
       const bool ok = (p < p_end) & (a_co[i] < a.Co);
-      glds16(ok ? (const void*)(DY + (size_t)p * a.lddy + a_co[i]) : (const void*)zero,
+      glds16(ok ? (const void*)(a_src[i] + (size_t)p * a_ld[i] + a_col[i]) : (const void*)zero,
              sA + (i * 8 + wave) * 1024);
     }
     // pixel decode of the K-step's first pixel (wave-uniform), then per-row carries
@@ -1200,7 +1207,8 @@ hipError_t wg2_launch(const WgradArgs& a, hipStream_t s) {
 
 bool conv_wgrad_v2_ok(const WgradArgs& a) {
   return (a.C % 8) == 0 && (a.ldx % 8) == 0 && (a.Co % 8) == 0 && (a.lddy % 8) == 0 &&
-         (long)a.N * a.Ho * a.Wo < (1L << 31);
+         (long)a.N * a.Ho * a.Wo < (1L << 31) &&
+         (!a.dy2 || (a.Co1 % 8 == 0 && a.Co1 < a.Co && a.lddy2 % 8 == 0));
 }
 
 // tile (BM co x BN cols): the largest the extents fill -- 256 x 256 (wave tiles 128 x 64)

@@ -1490,20 +1490,18 @@ int lbf_wgrad(Step& S, Unit& u, const Act& dyhat) {
   // (the combine is recorded with the BN-backward apply class, lbf_combine)
   const double gbx = (((double)P * L.co + (double)P * L.ci) * c->esz + (double)L.co * L.ci * 4.0) * 1e-9;
   if (int r = prof_begin(c, W.s, 2, li, 2.0 * P * L.co * L.ci * 1e-9, &slot, gbx)) return r;
-  if (L.ci < 256) {   // narrow ci: P1 and G as two weight-gradient launches of their own tile shapes
-    for (int part = 0; part < 2; ++part) {
-      WgradArgs a{};
-      a.dy = part ? y2.p : dyhat.p; a.lddy = part ? y2.ld : dyhat.ld;
-      a.x = y2.p; a.N = y2.N; a.H = y2.H; a.W = y2.W; a.C = y2.C; a.ldx = y2.ld;
-      a.Ho = L.Ho; a.Wo = L.Wo; a.Co = part ? L.ci : L.co;
-      a.KH = a.KW = 1; a.sf = 1; a.dil = 1;
-      const long n = (long)a.Co * a.C;
-      a.splits = wgrad_splits(a, S.dt, c->side_active);
-      a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / n));
-      a.out = c->slab;
-      HIPCALL(c, launch_conv_wgrad(S.dt, a, W.s));
-      HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, n, n, c->lbf_p1 + (part ? (size_t)L.co * L.ci : 0), 0, W.s));
-    }
+  if (L.ci < 256) {   // narrow ci: P1 and G as one launch of the tile shape the v2 heuristic picks
+    WgradArgs a{};
+    a.dy = dyhat.p; a.lddy = dyhat.ld;
+    a.dy2 = y2.p; a.lddy2 = y2.ld; a.Co1 = L.co;
+    a.x = y2.p; a.N = y2.N; a.H = y2.H; a.W = y2.W; a.C = y2.C; a.ldx = y2.ld;
+    a.Ho = L.Ho; a.Wo = L.Wo; a.Co = L.co + L.ci;
+    a.KH = a.KW = 1; a.sf = 1; a.dil = 1;
+    a.splits = wgrad_splits(a, S.dt, c->side_active);
+    a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / n1));
+    a.out = c->slab;
+    HIPCALL(c, launch_conv_wgrad(S.dt, a, W.s));
+    HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, n1, n1, c->lbf_p1, 0, W.s));
   } else {
     // P1 = dyhat^T y2 and G = y2^T y2 as one launch: output rows co.. co + ci - 1 take y2 as dy
     WgradArgs a{};
