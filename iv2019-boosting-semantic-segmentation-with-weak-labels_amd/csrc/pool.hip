@@ -167,6 +167,62 @@ __global__ __launch_bounds__(256) void maxpool_bwd_row_kernel(
   Vec8<T>::store(dx + ((size_t)((long)n * H + hi) * W + wi) * lddx + cg * 8, acc);
 }
 
+// tiled gather for the stem pool without padding (H = 2 Ho, W = 2 Wo, C = 64): a block owns
+// input rows 2r, 2r + 1 and 64 input columns; the pooled rows r - 1, r and the 33 pooled columns
+// that cover them are staged once in LDS (gradient + argmax bytes), so each pooled value is read
+// ~2x from L2 instead of ~9x (one thread per input pixel and 8 channels, every covering window
+// re-read); per pixel the same windows in the same order as maxpool_bwd_row_kernel
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_tile_kernel(
+    const uint8_t* __restrict__ arg, int H, int W, const T* __restrict__ dy, int Ho, int Wo,
+    int lddy, T* __restrict__ dx, int lddx) {
+  constexpr int C = 64, TW = 64, PW = TW / 2 + 1;
+  __shared__ uint4 gs[2][PW][8];
+  __shared__ uint2 as[2][PW][8];
+  const int n = blockIdx.y / Ho, r = blockIdx.y - n * Ho;
+  const int w0 = blockIdx.x * TW, wo0 = w0 / 2 - 1;   // pooled column of LDS slot 0
+  const int t = threadIdx.x;
+  for (int i = t; i < 2 * PW * 8; i += 256) {
+    const int cg = i & 7, slot = (i >> 3) % PW, rs = (i >> 3) / PW;
+    const int ho = r - 1 + rs, wo = wo0 + slot;
+    const bool ok = ho >= 0 && ho < Ho && wo >= 0 && wo < Wo;
+    const size_t q = ok ? (size_t)((long)n * Ho + ho) * Wo + wo : 0;
+    as[rs][slot][cg] = ok ? *(const uint2*)(arg + q * C + cg * 8) : make_uint2(~0u, ~0u);
+    gs[rs][slot][cg] = ok ? *(const uint4*)(dy + q * lddy + cg * 8) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int it = t + 256 * k;            // (row, col, cg): cg fastest, then column
+    const int cg = it & 7, pix = it >> 3;
+    const int ri = pix / TW, cj = pix - ri * TW;
+    const int hi = 2 * r + ri, wi = w0 + cj;
+    if (wi >= W) continue;
+    const int ho_lo = hi - 2 < 0 ? 0 : (hi - 1) >> 1, ho_hi = hi >> 1;
+    const int wo_lo = wi - 2 < 0 ? 0 : (wi - 1) >> 1, wo_hi = wi >> 1;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ho = ho_lo + i, wo = wo_lo + j;
+        if (ho > ho_hi || ho >= Ho || wo > wo_hi || wo >= Wo) continue;
+        const uint32_t me = (uint32_t)((hi - 2 * ho) * 3 + (wi - 2 * wo));
+        const uint2 a = as[ho - (r - 1)][wo - wo0][cg];
+        float g[8];
+        Half<T>::unpack(gs[ho - (r - 1)][wo - wo0][cg], g);
+        const uint32_t b[8] = {a.x & 255, (a.x >> 8) & 255, (a.x >> 16) & 255, a.x >> 24,
+                               a.y & 255, (a.y >> 8) & 255, (a.y >> 16) & 255, a.y >> 24};
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (b[e] == me) acc[e] += g[e];
+      }
+    Vec8<T>::store(dx + ((size_t)((long)n * H + hi) * W + wi) * lddx + cg * 8, acc);
+  }
+}
+
 template <typename T>
 __global__ void maxpool_bwd_kernel(const uint8_t* __restrict__ arg, int N, int H, int W, int C,
                                    const T* __restrict__ dy, int Ho, int Wo, int lddy,
@@ -512,6 +568,17 @@ hipError_t launch_maxpool_bwd(int dtype, const void* arg, int N, int H, int W, i
                               int pad_h, int pad_w, hipStream_t s) {
   if (C % 8 || lddy % 8 || lddx % 8) return hipErrorInvalidValue;
   if ((long)N * H * W * C / 8 >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit decode
+  if (C == 64 && pad_h == 0 && pad_w == 0 && H == 2 * Ho && W == 2 * Wo && (dtype == SEG_BF16 || dtype == SEG_F16) &&
+      (long)N * Ho < 65536) {   // the stem pool (16-bit): LDS-staged pooled tiles
+    dim3 g((unsigned)ceil_div(W, 64), (unsigned)(N * Ho));
+    if (dtype == SEG_BF16)
+      hipLaunchKernelGGL(maxpool_bwd_tile_kernel<bf16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, H, W,
+                         (const bf16_t*)dy, Ho, Wo, lddy, (bf16_t*)dx, lddx);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_tile_kernel<f16_t>, g, dim3(256), 0, s, (const uint8_t*)arg, H, W,
+                         (const f16_t*)dy, Ho, Wo, lddy, (f16_t*)dx, lddx);
+    return hipGetLastError();
+  }
   if (C == 64 && (long)N * H < 65536) {   // the stem pool: one row of the input per grid row
     dim3 g((unsigned)ceil_div((long)W * 8, 256), (unsigned)(N * H));
     if (dtype == SEG_BF16)
