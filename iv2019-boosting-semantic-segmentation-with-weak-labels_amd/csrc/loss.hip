@@ -5,8 +5,11 @@
 // footprint touches them (a halo of one low-res cell each side). The gradient w.r.t. the
 // low-res logits is the transpose of the separable resize: per full-res row the pixel
 // gradients are reduced along x into the owned columns (weights 1-xl / xl), then folded
-// into the owned rows (weights 1-yl / yl) held in registers. Loss sums and decisions are
-// produced only by the owner of a pixel (the block containing its top-left source corner).
+// into the owned rows (weights 1-yl / yl) held in registers -- or, when the block's columns fit
+// one chunk (C2: 249 of 256), each thread first sums its column over the rows into the owned
+// rows and the x-reduction runs once per owned row (YF; 409 -> 326 us per call at C2). Loss
+// sums and decisions are produced only by the owner of a pixel (the block containing its
+// top-left source corner).
 #include "loss.h"
 
 namespace {
@@ -16,6 +19,9 @@ namespace {
 #endif
 #ifndef LOSS_LB
 #define LOSS_LB 30
+#endif
+#ifndef LOSS_YF
+#define LOSS_YF 1   // A/B builds: 0 = the per-row x-reduction for every geometry
 #endif
 constexpr int LA = LOSS_LA;   // owned low-res rows per block
 constexpr int LB = LOSS_LB;   // owned low-res cols per block
@@ -48,7 +54,12 @@ __device__ int first_with_lo_ge(int target, int n_in, int n_out) {
   return o;
 }
 
-template <int C1, int C2, int C3>
+// YF (y first, the block's full-resolution columns fit one THREADS chunk): a thread keeps its
+// column's gradient summed over the rows into the LA owned low-res rows (weights 1-yl / yl) in
+// registers, and the x-transpose reduction into the owned columns runs once per owned row at the
+// end instead of once per full-resolution row (~32 LDS passes and barrier pairs per block). The
+// same products, summed h-then-w instead of w-then-h.
+template <int C1, int C2, int C3, int YF = 0>
 __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTables t) {
   constexpr int CT = C1 + C2 + C3;
   constexpr int WIN_R = LA + 2, WIN_C = LB + 2;
@@ -112,6 +123,12 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
 #pragma unroll
     for (int r = 0; r < LA; ++r) acc[u][r] = 0.f;
 
+  float colacc[YF ? LA : 1][YF ? CT : 1];
+#pragma unroll
+  for (int r = 0; r < (YF ? LA : 1); ++r)
+#pragma unroll
+    for (int c = 0; c < (YF ? CT : 1); ++c) colacc[r][c] = 0.f;
+
   float s1 = 0.f, s2v = 0.f, s2h = 0.f, c1n = 0.f, c2vn = 0.f, c2hn = 0.f;
   const bool strong = n < a.npp;
   const float* soft = nullptr;
@@ -119,6 +136,54 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
     soft = (n < a.npp + a.npb) ? a.bbox_soft + (size_t)(n - a.npp) * a.H * a.W * t.n_pb
                                : a.tag_soft + (size_t)(n - a.npp - a.npb) * a.H * a.W * t.n_pb;
   }
+
+  // x-reduction into the owned columns of one THREADS-wide chunk of gbuf (columns from wc):
+  // ra(j, c) += sum_w wx(w, j) gbuf(c, w)
+  auto xred = [&](int wc, float (&ra)[PPT]) {
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      const int pr = tid + THREADS * u;
+      if (pr < PAIRS) {
+        const int jj = pr / CT, c = pr % CT;
+        const int j = j0 + jj;
+        if (j < j_own_end) {
+          const int cend = min(w_end, wc + THREADS);
+          float sacc = 0.f;
+          // w with lo == j  -> weight (1 - xl) [+ xl if j is the clamped last column]
+          int wa = max(wstart[jj + 1], wc), wb = min(wstart[jj + 2], cend);
+          if (use_xt) {
+            // precomputed weights: one gbuf read + one broadcast table read per w
+            for (int w = wa; w < wb; ++w) sacc += gbuf[c * GLD + (w - wc)] * wa_t[w - w_begin];
+            wa = max(wstart[jj], wc);
+            wb = min(wstart[jj + 1], cend);
+            for (int w = wa; w < wb; ++w) sacc += gbuf[c * GLD + (w - wc)] * wb_t[w - w_begin];
+            ra[u] += sacc;
+            continue;
+          }
+          for (int w = wa; w < wb; ++w) {
+            int lo, hi;
+            float xl;
+            if (use_xt) { xl = xlt[w - w_begin]; lo = xlo_t[w - w_begin]; hi = xhi_t[w - w_begin]; }
+            else lerp_of(w, a.Wl, a.W, lo, hi, xl);
+            float gv = gbuf[c * GLD + (w - wc)];
+            sacc += gv * (1.f - xl);
+            if (hi == lo) sacc += gv * xl;
+          }
+          // w with lo == j-1 (hi == j) -> weight xl
+          wa = max(wstart[jj], wc);
+          wb = min(wstart[jj + 1], cend);
+          for (int w = wa; w < wb; ++w) {
+            int lo, hi;
+            float xl;
+            if (use_xt) { xl = xlt[w - w_begin]; lo = xlo_t[w - w_begin]; hi = xhi_t[w - w_begin]; }
+            else lerp_of(w, a.Wl, a.W, lo, hi, xl);
+            if (hi == j) sacc += gbuf[c * GLD + (w - wc)] * xl;
+          }
+          ra[u] += sacc;
+        }
+      }
+    }
+  };
 
   for (int h = h_begin; h < h_end; ++h) {
     int ylo, yhi;
@@ -276,70 +341,66 @@ __global__ __launch_bounds__(THREADS) void loss_head_kernel(LossArgs a, LossTabl
           }
         }
         // ---- gradients: TF xent backprop = p - y, times the weight ----
+        if constexpr (YF) {
+          float gv[CT];
 #pragma unroll
-        for (int c = 0; c < C1; ++c)
-          gbuf[c * GLD + tid] = strong ? w1 * (p[c] - (c == l1lab ? 1.f : 0.f)) : 0.f;
+          for (int c = 0; c < C1; ++c) gv[c] = strong ? w1 * (p[c] - (c == l1lab ? 1.f : 0.f)) : 0.f;
 #pragma unroll
-        for (int c = 0; c < C2; ++c) gbuf[(C1 + c) * GLD + tid] = w2 * (p[C1 + c] - y2[c]);
+          for (int c = 0; c < C2; ++c) gv[C1 + c] = w2 * (p[C1 + c] - y2[c]);
 #pragma unroll
-        for (int c = 0; c < C3; ++c) gbuf[(C1 + C2 + c) * GLD + tid] = w3 * (p[C1 + C2 + c] - y3[c]);
-      }
-      __syncthreads();
-      // ---- x-reduction into owned columns: rowacc(j) ----
+          for (int c = 0; c < C3; ++c) gv[C1 + C2 + c] = w3 * (p[C1 + C2 + c] - y3[c]);
 #pragma unroll
-      for (int u = 0; u < PPT; ++u) {
-        const int pr = tid + THREADS * u;
-        if (pr < PAIRS) {
-          const int jj = pr / CT, c = pr % CT;
-          const int j = j0 + jj;
-          if (j < j_own_end) {
-            const int cend = min(w_end, wc + THREADS);
-            float sacc = 0.f;
-            // w with lo == j  -> weight (1 - xl) [+ xl if j is the clamped last column]
-            int wa = max(wstart[jj + 1], wc), wb = min(wstart[jj + 2], cend);
-            if (use_xt) {
-              // precomputed weights: one gbuf read + one broadcast table read per w
-              for (int w = wa; w < wb; ++w) sacc += gbuf[c * GLD + (w - wc)] * wa_t[w - w_begin];
-              wa = max(wstart[jj], wc);
-              wb = min(wstart[jj + 1], cend);
-              for (int w = wa; w < wb; ++w) sacc += gbuf[c * GLD + (w - wc)] * wb_t[w - w_begin];
-              rowacc[u] += sacc;
-              continue;
-            }
-            for (int w = wa; w < wb; ++w) {
-              int lo, hi;
-              float xl;
-              if (use_xt) { xl = xlt[w - w_begin]; lo = xlo_t[w - w_begin]; hi = xhi_t[w - w_begin]; }
-              else lerp_of(w, a.Wl, a.W, lo, hi, xl);
-              float gv = gbuf[c * GLD + (w - wc)];
-              sacc += gv * (1.f - xl);
-              if (hi == lo) sacc += gv * xl;
-            }
-            // w with lo == j-1 (hi == j) -> weight xl
-            wa = max(wstart[jj], wc);
-            wb = min(wstart[jj + 1], cend);
-            for (int w = wa; w < wb; ++w) {
-              int lo, hi;
-              float xl;
-              if (use_xt) { xl = xlt[w - w_begin]; lo = xlo_t[w - w_begin]; hi = xhi_t[w - w_begin]; }
-              else lerp_of(w, a.Wl, a.W, lo, hi, xl);
-              if (hi == j) sacc += gbuf[c * GLD + (w - wc)] * xl;
-            }
-            rowacc[u] += sacc;
+          for (int r = 0; r < (YF ? LA : 1); ++r) {
+            const int i = i0 + r;
+            if (i == ylo)
+#pragma unroll
+              for (int c = 0; c < CT; ++c) colacc[r][c] += gv[c] * (1.f - yl);
+            if (i == yhi)
+#pragma unroll
+              for (int c = 0; c < CT; ++c) colacc[r][c] += gv[c] * yl;
           }
+        } else {
+#pragma unroll
+          for (int c = 0; c < C1; ++c)
+            gbuf[c * GLD + tid] = strong ? w1 * (p[c] - (c == l1lab ? 1.f : 0.f)) : 0.f;
+#pragma unroll
+          for (int c = 0; c < C2; ++c) gbuf[(C1 + c) * GLD + tid] = w2 * (p[C1 + c] - y2[c]);
+#pragma unroll
+          for (int c = 0; c < C3; ++c) gbuf[(C1 + C2 + c) * GLD + tid] = w3 * (p[C1 + C2 + c] - y3[c]);
         }
       }
+      if constexpr (YF) continue;   // (one chunk: wc == w_begin)
+      __syncthreads();
+      xred(wc, rowacc);
       __syncthreads();
     }
     // ---- fold the row into owned low-res rows ----
+    if constexpr (!YF) {
 #pragma unroll
-    for (int u = 0; u < PPT; ++u) {
+      for (int u = 0; u < PPT; ++u) {
 #pragma unroll
-      for (int r = 0; r < LA; ++r) {
-        const int i = i0 + r;
-        if (i == ylo) acc[u][r] += rowacc[u] * (1.f - yl);
-        if (i == yhi) acc[u][r] += rowacc[u] * yl;
+        for (int r = 0; r < LA; ++r) {
+          const int i = i0 + r;
+          if (i == ylo) acc[u][r] += rowacc[u] * (1.f - yl);
+          if (i == yhi) acc[u][r] += rowacc[u] * yl;
+        }
       }
+    }
+  }
+  if constexpr (YF) {   // the column sums of each owned row through the x-reduction, once
+#pragma unroll
+    for (int r = 0; r < (YF ? LA : 1); ++r) {
+      if (w_begin + tid < w_end)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) gbuf[c * GLD + tid] = colacc[r][c];
+      __syncthreads();
+      float ra[PPT];
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) ra[u] = 0.f;
+      xred(w_begin, ra);
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) acc[u][r] = ra[u];
+      __syncthreads();
     }
   }
   // ---- write owned gradient ----
@@ -648,7 +709,13 @@ int loss_head_blocks(int N, int Hl, int Wl) {
 
 hipError_t launch_loss_head(const LossArgs& a, const LossTables& t, hipStream_t s) {
   dim3 g(loss_head_blocks(a.N, a.Hl, a.Wl));
-  if (t.c1 == 14 && t.c2 == 7 && t.c3 == 3)
+  // y-first accumulation when every block's full-resolution columns fit one chunk: (LB + 1)
+  // low-res cells of (W - 1) / (Wl - 1) columns each, plus the two boundary columns
+  const double span = a.Wl > 1 ? (LB + 1) * (double)(a.W - 1) / (double)(a.Wl - 1) + 3.0 : 1e9;
+  const bool yf = LOSS_YF && span <= THREADS;
+  if (t.c1 == 14 && t.c2 == 7 && t.c3 == 3 && yf)
+    hipLaunchKernelGGL((loss_head_kernel<14, 7, 3, 1>), g, dim3(THREADS), 0, s, a, t);
+  else if (t.c1 == 14 && t.c2 == 7 && t.c3 == 3)
     hipLaunchKernelGGL((loss_head_kernel<14, 7, 3>), g, dim3(THREADS), 0, s, a, t);
   else if (t.c1 == 53 && t.c2 == 12 && t.c3 == 5)
     hipLaunchKernelGGL((loss_head_kernel<53, 12, 5>), g, dim3(THREADS), 0, s, a, t);
