@@ -365,7 +365,24 @@ __global__ __launch_bounds__(256) void grid_rowreduce8_kernel(const T* __restric
         tab[q * 256 + w] = g.rowtab[(size_t)(q0 + q) * W + w0 + w];
       }
       __syncthreads();
-      for (int w = rl; w < wn; w += RL) {
+      // a lane's pixels 4 at a time: the 4 loads issued before their (in-order) FMAs
+      int w = rl;
+      for (; w + 3 * RL < wn; w += 4 * RL) {
+        float v[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Vec8<T>::load(row + (size_t)(w0 + w + u * RL) * ldx, v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < QB; ++q) {
+            if (q < nq) {
+              const float wq = tab[q * 256 + w + u * RL];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) acc[q][e] = __builtin_fmaf(wq, v[u][e], acc[q][e]);
+            }
+          }
+      }
+      for (; w < wn; w += RL) {
         float v[8];
         Vec8<T>::load(row + (size_t)(w0 + w) * ldx, v);
 #pragma unroll
