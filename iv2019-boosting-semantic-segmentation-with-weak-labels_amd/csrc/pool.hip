@@ -484,6 +484,13 @@ __global__ void resize_fwd_kernel(const T* __restrict__ x, int N, int hi_n, int 
     const unsigned un = ut / (unsigned)Ho;
     const int ho = (int)(ut - un * (unsigned)Ho);
     const int n = (int)un;
+    if (hi_n == 1 && wi_n == 1) {   // 1 x 1 source (the image-pool branch): a broadcast, one
+                                    // load (every tap is the same cell, every weight 0)
+      float v[8];
+      Vec8<T>::load(x + (size_t)n * ldx + cg * 8, v);
+      Vec8<T>::store(y + (size_t)p * ldy + cg * 8, v);
+      continue;
+    }
     int y0, y1, x0, x1;
     float yl, xl;
     tf_lerp(ho, hi_n, Ho, y0, y1, yl);
