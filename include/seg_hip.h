@@ -114,9 +114,8 @@ int seg_set_nesterov(seg_ctx* ctx, int on);
  * running on the weight-gradient stream; seg_apply_update updates every other parameter beside
  * it and joins before the stem's weights. Every other call that takes a stream joins first.
  * No reference counterpart (scheduling only; results are unchanged). Off by default.
- * With on, seg_backward also defers every other layer's split-K weight-gradient reduce: they
- * run as one batched launch at the start of seg_apply_update (bitwise the same gradients);
- * seg_flush_grads runs them on `stream` for a caller that reads the gradient buffer first. */
+ * seg_flush_grads makes `stream` wait for that last weight gradient, for a caller that reads
+ * the gradient buffer before seg_apply_update. */
 int seg_set_defer_stem(seg_ctx* ctx, int on);
 int seg_flush_grads(seg_ctx* ctx, void* stream);
 /* pre-masked identity-unit gradients (on by default): when an identity unit follows another,
@@ -125,14 +124,18 @@ int seg_flush_grads(seg_ctx* ctx, void* stream);
  * Scheduling of bytes only: results are bitwise identical either way (tests/test_gpu_step.py).
  * No reference counterpart. */
 int seg_set_premask(seg_ctx* ctx, int on);
+/* linear BN-backward fold (on by default): the training BN backward of a 16-bit bottleneck's
+ * expanding conv3 is affine in the gated output gradient and in the conv input, so its apply
+ * pass is folded into the conv3 data gradient (a K-concatenated GEMM) and weight gradient
+ * (a second GEMM + an fp32 combine); 0 runs the separate BN-backward apply pass (the fold's
+ * reference path in the parity tests). Same math, different rounding order. No reference
+ * counterpart. */
+int seg_set_lbf(seg_ctx* ctx, int on);
 /* runtime counters since seg_create (diagnostics; no reference counterpart):
  * "premask_launches" = data gradients stored pre-masked (seg_set_premask): identity units'
  *   conv1, and at block boundaries a projection unit's conv1 + shortcut and decrease_fdims';
- * "bn_fold_launches" = data gradients whose epilogue also ran the consumer BN's backward
- * reduce (SEG_BN_FOLD=1 at seg_create);
  * "lbf_layers" = conv3 layers whose BN-backward apply was folded into their data / weight
- * gradients by linearity (16-bit identity units with an expanding conv3; SEG_LBF=0 at
- * seg_create turns it off). -ENOENT for an unknown name. */
+ * gradients by linearity (seg_set_lbf). -ENOENT for an unknown name. */
 int seg_counter(seg_ctx* ctx, const char* name, int64_t* value);
 
 /* outputs ------------------------------------------------------------------------------

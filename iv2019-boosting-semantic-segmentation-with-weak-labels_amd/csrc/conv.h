@@ -39,17 +39,6 @@ struct ConvArgs {
   // outputs whose bit is 0 are stored as zero (conv_nt_omask_ok launches only)
   const uint8_t* omask;
   int ldm;
-  // optional BN-backward reduce of the layer whose output gradient this data gradient is
-  // (ping-pong one-tile launches, no residual): per 256-row tile and channel the partial
-  // (sum dyhat, sum dyhat * xhat) with dyhat = out * ReLU bit, xhat = (bq_y - mean) * invstd,
-  // into bq_part [tiles][Co][2] (the separate bn_bwd_reduce8 pass's input, folded)
-  const void* bq_y;
-  int bq_ldy;
-  const uint8_t* bq_mask;
-  int bq_ldm;
-  const float* bq_mean;
-  const float* bq_invstd;
-  float* bq_part;
 };
 
 struct WgradArgs {
@@ -71,10 +60,6 @@ struct WgradArgs {
 // host launchers (conv.hip); return hipError_t
 hipError_t launch_conv_nt(int dtype, int out_f32, const ConvArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad(int dtype, const WgradArgs& a, hipStream_t s);
-// every deferred split-K reduce of a step in one launch (blockIdx.y = job); per element the
-// same slab-order sum as launch_splitk_reduce (bitwise-identical gradients)
-struct ReduceJob { const float* part; float* out; long n, stride; int splits; };
-hipError_t launch_splitk_reduce_batched(const ReduceJob* jobs, int njobs, hipStream_t s);
 hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride, long n,
                                 float* out, int accumulate, hipStream_t s);
 // all layers' flips in one launch: table of FlipJob (device), prefix = the job's first tile;
@@ -85,8 +70,8 @@ hipError_t launch_weight_flip_batched(int dtype, const FlipJob* jobs, int njobs,
                                       hipStream_t s);
 hipError_t launch_weight_flip_transpose(int dtype, const void* w, void* wt, int co, int kh, int kw,
                                         int ci, hipStream_t s);
-int conv_nt_mtiles(long M);  // upper bound on BN-stat partial tiles (64-row tiles)
-// rows per BN-stat partial tile of the kernel launch_conv_nt will pick (64, 128 or 256)
+int conv_nt_mtiles(long M);  // upper bound on BN-stat partial tiles (128-row tiles)
+// rows per BN-stat partial tile of the kernel launch_conv_nt will pick (128 or 256)
 int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a);
 bool conv_nt_v2_ok(const ConvArgs& a);
 int conv_nt_v2_rows(const ConvArgs& a);   // tile rows (= BN-stat partial rows) of the v2 config
@@ -103,16 +88,10 @@ hipError_t launch_conv_skinny(int dtype, const ConvArgs& a, hipStream_t s);
 // ping-pong 256x256 main loop (conv_pp.hip) for the v2 cases with Co > 128
 bool conv_nt_pp_ok(const ConvArgs& a);
 hipError_t launch_conv_nt_pp(int dtype, const ConvArgs& a, hipStream_t s);
-// short-K dense 1x1 with double-buffered accumulators (conv_db.hip): 256 x 128 tiles, the
-// epilogue of one tile inside the next tile's main loop; BN partials per 64 rows
-bool conv_nt_db_ok(const ConvArgs& a);
-hipError_t launch_conv_nt_db(int dtype, const ConvArgs& a, hipStream_t s);
 // launches that apply ConvArgs::omask: 16-bit dense 1x1 ping-pong, one tile per workgroup (the
 // identity units' conv1 data gradient with its residual; a projection unit's K-concatenated
 // conv1 + shortcut data gradient; decrease_fdims' data gradient into block4)
 bool conv_nt_omask_ok(int dtype, const ConvArgs& a);
-// launches that can fold the BN-backward reduce (ConvArgs::bq_*) into the epilogue
-bool conv_nt_bq_ok(int dtype, const ConvArgs& a);
 // ping-pong 256x256 weight gradient (conv_pp.hip), used when the v2 tile choice is 256 x 256
 bool conv_wgrad_pp_ok(const WgradArgs& a);
 hipError_t launch_conv_wgrad_pp(int dtype, const WgradArgs& a, hipStream_t s);

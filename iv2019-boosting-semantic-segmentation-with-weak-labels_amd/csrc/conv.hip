@@ -511,35 +511,6 @@ __global__ __launch_bounds__(NT_THREADS, 2) void conv_wgrad_kernel(WgradArgs a) 
     }
 }
 
-__global__ void splitk_reduce_batched_kernel(const ReduceJob* __restrict__ jobs) {
-  const ReduceJob j = jobs[blockIdx.y];
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t * 4 < j.n; t += (long)gridDim.x * blockDim.x) {
-    const long i4 = t * 4;
-    if (i4 + 3 < j.n && (j.stride & 3) == 0) {
-      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-      int z = 0;
-      for (; z + 8 <= j.splits; z += 8) {
-        float4 v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = *(const float4*)(j.part + (size_t)(z + k) * j.stride + i4);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
-      }
-      for (; z < j.splits; ++z) {
-        const float4 v = *(const float4*)(j.part + (size_t)z * j.stride + i4);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-      *(float4*)(j.out + i4) = s;
-    } else {
-      for (long i = i4; i < j.n && i < i4 + 4; ++i) {
-        float s = 0.f;
-        for (int z = 0; z < j.splits; ++z) s += j.part[(size_t)z * j.stride + i];
-        j.out[i] = s;
-      }
-    }
-  }
-}
-
 __global__ void splitk_reduce_kernel(const float* __restrict__ part, int splits, long stride,
                                      long n, float* __restrict__ out, int accumulate) {
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t * 4 < n; t += (long)gridDim.x * blockDim.x) {
@@ -663,7 +634,7 @@ hipError_t wg_dispatch(const WgradArgs& a, hipStream_t s) {
 
 }  // namespace
 
-int conv_nt_mtiles(long M) { return ceil_div(M, 64); }   // 64-row partials: conv_nt_db
+int conv_nt_mtiles(long M) { return ceil_div(M, 128); }
 
 int conv_nt_stat_rows(int dtype, int out_f32, const ConvArgs& a) {
   return (seg_half(dtype) && !out_f32 && conv_nt_v2_ok(a)) ? conv_nt_v2_rows(a) : 128;
@@ -844,13 +815,6 @@ hipError_t launch_splitk_reduce(const float* part, int splits, long split_stride
   return hipGetLastError();
 }
 
-hipError_t launch_splitk_reduce_batched(const ReduceJob* jobs, int njobs, hipStream_t s) {
-  if (njobs <= 0) return hipSuccess;
-  // 64 grid-stride workgroups per job: ~70 jobs fill the chip once (the largest layer, 2.4 M
-  // weights, is 36 float4 per thread)
-  hipLaunchKernelGGL(splitk_reduce_batched_kernel, dim3(64, njobs), dim3(256), 0, s, jobs);
-  return hipGetLastError();
-}
 
 hipError_t launch_weight_flip_batched(int dtype, const FlipJob* jobs, int njobs, long total,
                                       hipStream_t s) {

@@ -119,8 +119,7 @@ __device__ __forceinline__ void row_total8(float (&v)[8]) {
 
 // PERSIST: 1 = loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
 // epilogue; 0 = one tile per workgroup (the residual-epilogue launches: their register
-// budget goes to the residual prefetch instead of the next tile's address state); 2 = one tile
-// per workgroup whose epilogue also folds the consumer BN's backward reduce (ConvArgs::bq_*)
+// budget goes to the residual prefetch instead of the next tile's address state)
 template <typename E, int ST, int PERSIST>
 __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   typedef typename Half<E>::V V;
@@ -579,30 +578,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     const E* R1 = (const E*)a.r;
     const E* R2 = (const E*)a.r2;
     const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
-    // PERSIST == 2: the consumer BN's backward reduce over this tile (bn_bwd_reduce8's sums,
-    // folded): per thread its 8 rows x 8 channels of the rounded output, masked by the BN's
-    // ReLU bits, against x-hat of the BN input y; lanes of one channel group summed by
-    // shuffles, the 8 waves through LDS (after the last half), one (sum, sum*xhat) per tile
-    constexpr bool BQ = PERSIST == 2;
-    float bq_t1[8], bq_t2[8];
-    float* const bq_red = (float*)(smem + PP_LDS);   // [2 halves][8 waves][16 groups][8][2]
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn) {
       u32x4_t rs1[8], rs2[8];
-      uint32_t bqm[2];   // the 8 rows' ReLU bytes, 4 per register
-      if constexpr (BQ) {   // the BN input rows and ReLU bytes, issued before the staging
-        bqm[0] = bqm[1] = 0u;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const long m = m0 + k * 32 + s_row;
-          const long mc = m < M ? m : M - 1;
-          const int n = n0 + qn * 128 + s_ch * 8;
-          const int nc = n < a.Co ? n : 0;
-          rs1[k] = *(const u32x4_t*)((const E*)a.bq_y + (size_t)mc * a.bq_ldy + nc);
-          const uint32_t byte = m < M && n < a.Co ? a.bq_mask[(size_t)mc * a.bq_ldm + (nc >> 3)] : 0u;
-          bqm[k >> 2] |= byte << (8 * (k & 3));
-        }
-      }
       if (nres) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -656,50 +634,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             v[k][w] &= ((b & 1u) ? 0x0000ffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
           }
       }
-      if constexpr (BQ) {
-        const int nb = n0 + qn * 128 + s_ch * 8;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { bq_t1[e] = 0.f; bq_t2[e] = 0.f; }
-        // 4 channels at a time (their mean / invstd in 8 registers)
-#pragma unroll
-        for (int wh = 0; wh < 2; ++wh) {
-          float mu[4], inv[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int n = nb + wh * 4 + e;
-            mu[e] = n < a.Co ? a.bq_mean[n] : 0.f;
-            inv[e] = n < a.Co ? a.bq_invstd[n] : 0.f;
-          }
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-#pragma unroll
-            for (int w2 = 0; w2 < 2; ++w2) {
-              const int w = wh * 2 + w2;
-              const uint32_t b = bqm[k >> 2] >> (8 * (k & 3) + 2 * w);
-              const float d0 = (b & 1u) ? TypeOps<E>::to_f(lo16<E>(v[k][w])) : 0.f;
-              const float d1 = (b & 2u) ? TypeOps<E>::to_f(hi16<E>(v[k][w])) : 0.f;
-              const float x0 = (TypeOps<E>::to_f(lo16<E>(rs1[k][w])) - mu[2 * w2]) * inv[2 * w2];
-              const float x1 = (TypeOps<E>::to_f(hi16<E>(rs1[k][w])) - mu[2 * w2 + 1]) * inv[2 * w2 + 1];
-              bq_t1[2 * w] += d0;
-              bq_t2[2 * w] += d0 * x0;
-              bq_t1[2 * w + 1] += d1;
-              bq_t2[2 * w + 1] += d1 * x1;
-            }
-        }
-        // the 4 row groups of the wave holding this channel group (lanes s_ch + 16 q)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          bq_t1[e] += __shfl_xor(bq_t1[e], 16, 64);
-          bq_t2[e] += __shfl_xor(bq_t2[e], 16, 64);
-          bq_t1[e] += __shfl_xor(bq_t1[e], 32, 64);
-          bq_t2[e] += __shfl_xor(bq_t2[e], 32, 64);
-        }
-        if ((tid & 63) < 16) {
-          float* r = bq_red + ((qn * 8 + (tid >> 6)) * 16 + s_ch) * 16;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { r[2 * e] = bq_t1[e]; r[2 * e + 1] = bq_t2[e]; }
-        }
-      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const long m = m0 + k * 32 + s_row;
@@ -708,22 +642,6 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       if (qn == 0) {   // the second half overwrites the staging area
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         pp_barrier();
-      }
-    }
-    if constexpr (BQ) {   // the 8 waves' partials, fixed order: one (sum, sum*xhat) per channel
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      pp_barrier();
-      if (tid < 256) {
-        const int hq = tid >> 7, ch = tid & 127;
-        const int n = n0 + hq * 128 + ch;
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-          const float* r = bq_red + ((hq * 8 + w) * 16 + (ch >> 3)) * 16 + 2 * (ch & 7);
-          s1 += r[0];
-          s2 += r[1];
-        }
-        if (n < a.Co) *(float2*)(a.bq_part + 2 * ((size_t)mt * a.Co + n)) = make_float2(s1, s2);
       }
     }
   }
@@ -757,8 +675,8 @@ int pp_grid(int nwg) {
 
 template <typename E, int ST, int PERSIST>
 hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
-  // two K-tile buffers (the epilogue stages through buffer 1) + the BN-reduce partials
-  constexpr int LDS = PP_LDS + (PERSIST == 2 ? 2 * 8 * 16 * 16 * 4 : 0);
+  // two K-tile buffers (the epilogue stages through buffer 1)
+  constexpr int LDS = PP_LDS;
   auto kern = conv_nt_pp_kernel<E, ST, PERSIST>;
   static bool attr = false;
   if (!attr) {
@@ -774,10 +692,6 @@ hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
 
 template <typename E, int ST>
 hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
-  if (a.bq_part) {
-    if constexpr (ST == 0 || ST == 1) return pp_launch<E, ST, 2>(a, s);
-    return hipErrorInvalidValue;
-  }
   if (a.r || a.r2 || a.omask) return pp_launch<E, ST, 0>(a, s);
   return pp_launch<E, ST, 1>(a, s);
 }
@@ -796,11 +710,6 @@ bool conv_nt_pp_ok(const ConvArgs& a) {
                     a.H == a.Ho && a.W == a.Wo && a.C % 64 == 0 && a.C2 % 64 == 0 && a.ldx2 % 8 == 0 &&
                     a.ldw2 % 8 == 0 && (long)a.N * a.H * a.W * a.ldx2 * 2 < (1L << 31) &&
                     (long)a.Co * a.ldw2 * 2 < (1L << 31) && !a.r && !a.r2));
-}
-
-bool conv_nt_bq_ok(int dtype, const ConvArgs& a) {
-  return seg_half(dtype) && !a.tap8 && a.st == 1 && !a.x2 && !a.r && !a.r2 && !a.omask &&
-         !a.stats && a.Co > 128 && conv_nt_pp_ok(a);
 }
 
 bool conv_nt_omask_ok(int dtype, const ConvArgs& a) {

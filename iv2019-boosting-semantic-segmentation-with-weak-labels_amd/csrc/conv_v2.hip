@@ -891,9 +891,7 @@ bool conv_nt_v2_ok(const ConvArgs& a) {
 static bool v2_small_tile(const ConvArgs& a) { return a.Co <= 64; }
 
 int conv_nt_v2_rows(const ConvArgs& a) {
-  // the short-K kernel writes one partial per wave (64 rows), the ping-pong kernel one per wave
-  // row (128 rows), the v2 kernels one per tile
-  if (a.Co > 128 && conv_nt_db_ok(a)) return 64;
+  // the ping-pong kernel writes one partial per wave row (128 rows), the v2 kernels one per tile
   if (a.Co > 128 && !a.r && !a.r2 && conv_nt_pp_ok(a)) return 128;
   if (conv_nt_patch_ok(a) || conv_nt_patch_s2d_ok(a)) return 256;
   return v2_small_tile(a) ? 128 : 256;
@@ -923,7 +921,6 @@ hipError_t v2_dispatch(int dtype, const ConvArgs& a, hipStream_t s) {
     return patch_launch<E, 64, 8, 1, 1, 3, 2>(a, s);
   }
   if (a.Co > 128) {
-    if (conv_nt_db_ok(a)) return launch_conv_nt_db(dtype, a, s);
     if (conv_nt_pp_ok(a)) return launch_conv_nt_pp(dtype, a, s);
     return v2_launch<E, 256, 4, 2, 2, ST>(a, s);
   }

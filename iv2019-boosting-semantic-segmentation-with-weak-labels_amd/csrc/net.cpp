@@ -62,10 +62,6 @@ struct ConvL {
   float* stats_part = nullptr;    // [mtiles][co][2]
   float* bwd_part = nullptr;      // [rb][co][2] (group norm: [N][rb][co][2], rb per image)
   int rb = 1;
-  // the BN-backward reduce folded into the producing data gradient's epilogue (round 5,
-  // ConvArgs::bq_*): per 256-row tile partials [ceil(M/256)][co][2]; nullptr = not foldable
-  float* bq_part = nullptr;
-  bool bq_ready = false;          // this step's partials were written by the data gradient
   // linear BN-backward fold (lbf.h; an identity unit's expansion conv3): per-channel (A, B, D)
   // [3][co] of the last backward, the gated gradient it read (seg_debug_tensor materialises dy
   // from it on request: the step itself never writes dy of such a layer)
@@ -216,7 +212,6 @@ struct seg_ctx {
   bool defer_stem = false;
   bool premask = true;             // seg_set_premask: pre-masked identity-unit gradients (unit_backward)
   int64_t premask_launches = 0;    // conv1 data gradients stored pre-masked (seg_counter)
-  int64_t bq_launches = 0;         // data gradients with the BN-backward reduce folded (seg_counter)
   bool prestem_rec = false;
   bool stem_pending = false;
   float* dzscale = nullptr;       // [ldl]
@@ -225,24 +220,12 @@ struct seg_ctx {
   // workspace
   float* slab = nullptr;
   size_t slab_floats = 0;
-  // deferred split-K reduces (round 5): with seg_set_defer_stem (one process: nothing reads the
-  // gradients between backward and update) every weight gradient but the stem's writes its own
-  // slab region and ALL their reduces run as one launch at the start of seg_apply_update (or
-  // seg_flush_grads), instead of one reduce per layer on the weight-gradient stream beside the
-  // data-gradient chain
-  float* slab_all = nullptr;
-  std::vector<long> slab_off;      // per conv: its region in slab_all (-1 = none)
-  std::vector<long> slab_cap;      // per conv: floats in that region
-  ReduceJob* red_jobs = nullptr;   // device table, one job per deferred layer (jobs built per step)
-  std::vector<ReduceJob> red_host, red_dev;   // this step's jobs / the device table's copy
-  bool defer_red_on = false;       // SEG_DEFER_REDUCE=1 at creation: on (A/B; -0.8 % step)
-  // linear BN-backward fold (lbf.h), on unless SEG_LBF=0 at creation: 16-bit identity units
-  // whose conv3 expands (co >= 2 ci, ci > 128: blocks 3-4). Compute-stream scratch (used in
+  // linear BN-backward fold (lbf.h), on unless seg_set_lbf(ctx, 0): 16-bit bottleneck units
+  // whose conv3 expands (co >= 2 ci, ci % 64 == 0: every unit of R50). Compute-stream scratch (used in
   // order by one layer at a time): the scaled data-gradient weights, the D-scaled weights, H
   // and its split-K slab, the data gradient's constant; weight-gradient-stream scratch: the
   // two GEMM results and the column-sum partials of the conv input
-  bool lbf_on = false;
-  bool lbf_late = false;           // SEG_LBF_LATE=1 (A/B): side-stream work after the data gradient
+  bool lbf_on = true;
   void* lbf_wts = nullptr;
   void* lbf_xd = nullptr;
   void* lbf_h = nullptr;
@@ -251,9 +234,6 @@ struct seg_ctx {
   float* lbf_bpart = nullptr;
   float* lbf_p1 = nullptr;
   int64_t lbf_launches = 0;        // layers folded (seg_counter)
-  bool bq_on = false;              // SEG_BN_FOLD=1 at creation: BN-backward reduce folded (A/B; -1.3 %)
-  bool defer_red = false;          // this step's non-stem reduces are deferred
-  bool red_pending = false;        // ... and have not run yet
   float* stat_scratch = nullptr;
   size_t stat_scratch_floats = 0;
   Prof prof;
@@ -459,8 +439,6 @@ int alloc_conv(seg_ctx* c, ConvL& L, int N, int H, int W, int ldy = 0) {
     if (int r = dalloc(c, &L.st_dev, (size_t)N)) return r;
     HIPCALL(c, hipMemcpy(L.st_dev, L.st_img.data(), N * sizeof(BnState), hipMemcpyHostToDevice));
   } else {
-    if (L.co > 128 && seg_half(c->dt))   // the ping-pong data gradients' width (Co > 128)
-      if (int r = dalloc(c, &L.bq_part, (size_t)ceil_div(M, 256) * L.co * 2)) return r;
     L.rb = bn_bwd_rowblocks(M, L.co);
     if (int r = dalloc(c, &L.bwd_part, (size_t)L.rb * L.co * 2)) return r;
   }
@@ -676,19 +654,13 @@ int bn_backward(Step& S, int li, const Act& dz, int dz_f32, const Act* z, const 
   const double me = a.M * (double)a.C * 1e-9;
   const double gb_in = me * (zsz + (a.mask ? 0.125 : (z ? zsz : 0.0)) + esz);
   int slot;
-  // folded (conv_dgrad with bn_li): the data gradient's epilogue already wrote the partials
-  const bool folded = L.bq_ready;
-  L.bq_ready = false;
-  if (!folded) {
-    if (int r = prof_begin(c, S.s, 4, li, gb_in + (a.reduce_dyhat ? me * esz : 0.0), &slot)) return r;
-    HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
-    if (int r = prof_end(c, S.s, slot)) return r;
-  }
+  if (int r = prof_begin(c, S.s, 4, li, gb_in + (a.reduce_dyhat ? me * esz : 0.0), &slot)) return r;
+  HIPCALL(c, launch_bn_bwd_reduce(S.dt, dz_f32, a, S.s));
+  if (int r = prof_end(c, S.s, slot)) return r;
   const bool tb = c->cfg.train_bn != 0;
   // a backward after a moving-statistics forward (TRAIN without
   // batch_norm_accumulate_statistics) differentiates through constant statistics
-  HIPCALL(c, launch_bn_bwd_finalize(folded ? L.bq_part : L.bwd_part,
-                                    folded ? ceil_div(a.M, 256) : L.rb, a.M, L.co, L.st,
+  HIPCALL(c, launch_bn_bwd_finalize(L.bwd_part, L.rb, a.M, L.co, L.st,
                                     tb ? c->grads + L.g_off : nullptr,
                                     tb ? c->grads + L.b_off : nullptr, S.s, c->bn_infer));
   if (c->sync_fn && !c->bn_infer) {
@@ -811,25 +783,13 @@ int gn_backward(Step& S, int li, const Act& dz0, int dz_f32, const Act* z0, cons
 // dx = dgrad(dy) [+ r1] [+ r2]
 ConvArgs dgrad_args(seg_ctx* c, int li, const Act& dx, const Act* r1, const Act* r2);
 
-// dx = dgrad(dy) [+ r1] [+ r2]
-// bn_li / bn_z: the BN layer whose output gradient dx is, and its output activation (the ReLU
-// bits): with seg_ctx::bq_on the BN-backward reduce is folded into this data gradient's
-// epilogue where the one-tile ping-pong launch can take it (then bn_backward skips its reduce)
+// dx = dgrad(dy) [+ r1] [+ r2]; omask: ReLU bits to store dx masked by (premask)
 int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Act* r2 = nullptr,
-               const uint8_t* omask = nullptr, int bn_li = -1, const Act* bn_z = nullptr) {
+               const uint8_t* omask = nullptr) {
   seg_ctx* c = S.c;
   ConvL& L = c->convs[li];
   ConvArgs a = dgrad_args(c, li, dx, r1, r2);
   if (omask) { a.omask = omask; a.ldm = a.Co / 8; }
-  if (bn_li >= 0 && c->bq_on && !c->gn && bn_z && bn_z->mask) {
-    ConvL& B = c->convs[bn_li];
-    if (B.bq_part && bn_z->C == B.co && B.co == a.Co && B.y.M() == dx.M() && conv_nt_bq_ok(S.dt, a)) {
-      a.bq_y = B.y.p; a.bq_ldy = B.y.ld; a.bq_mask = bn_z->mask; a.bq_ldm = (B.co + 7) / 8;
-      a.bq_mean = B.st.mean; a.bq_invstd = B.st.invstd; a.bq_part = B.bq_part;
-      B.bq_ready = true;
-      ++c->bq_launches;
-    }
-  }
   long M = (long)L.N * L.H * L.W;
   int slot;
   // dy + w + dx (+ each residual read once)
@@ -838,8 +798,7 @@ int conv_dgrad(Step& S, int li, const Act& dx, const Act* r1 = nullptr, const Ac
                       (double)M * L.ci * (1.0 + nres)) * c->esz * 1e-9;
   if (int r = prof_begin(c, S.s, 1, li, 2.0 * M * L.ci * L.k * L.k * L.co * 1e-9 / L.stride / L.stride,
                          &slot, gbx)) return r;
-  if (a.bq_part) HIPCALL(c, launch_conv_nt_pp(S.dt, a, S.s));
-  else HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
+  HIPCALL(c, launch_conv_nt(S.dt, 0, a, S.s));
   return prof_end(c, S.s, slot);
 }
 
@@ -906,7 +865,6 @@ int bucket_progress(seg_ctx* c, hipStream_t ws, bool final) {
 }
 
 int conv_wgrad_impl(Step& S, int li, const Act& x);
-int flush_reduces(seg_ctx* c, hipStream_t s);
 int conv_wgrad(Step& S, int li, const Act& x) {
   seg_ctx* c = S.c;
   Step W = S;
@@ -939,12 +897,9 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   // ~0.75 ms waiting for it)
   a.splits = wgrad_splits(a, S.dt, c->side_active && li != c->stem);
   const long per = (long)a.Co * a.KH * a.KW * a.C;
-  // deferred reduce: this layer's own slab region, the reduce joins the step's batched one
-  const bool defer = c->defer_red && li != c->stem && !s2d && c->slab_off[li] >= 0 &&
-                     (long)a.splits * per <= c->slab_cap[li];
-  if (!defer)  // the shared slab was sized at creation for these shapes; never exceed it
-    a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / per));
-  a.out = defer ? c->slab_all + c->slab_off[li] : c->slab;
+  // the shared slab was sized at creation for these shapes; never exceed it
+  a.splits = (int)std::max<long>(1, std::min<long>(a.splits, (long)c->slab_floats / per));
+  a.out = c->slab;
   long P = (long)L.N * L.Ho * L.Wo;
   int slot;
   // dy + x (16-bit) + the fp32 weight gradient; split-K slab traffic is overhead, not algorithmic
@@ -961,11 +916,6 @@ int conv_wgrad_impl(Step& S, int li, const Act& x) {
   const long n = (long)L.co * L.k * L.k * L.ci;
   // slab rows are co_pad wide only in the Co dimension: rows 0..co-1 are the real ones
   // split z of the slab starts at z*co_pad*ncol; rows >= co are padding and never reduced
-  if (defer) {
-    c->red_host.push_back({a.out, c->grads + L.w_off, n, (long)L.co_pad * L.k * L.k * L.ci, a.splits});
-    c->red_pending = true;
-    return 0;
-  }
   HIPCALL(c, launch_splitk_reduce(c->slab, a.splits, (long)L.co_pad * L.k * L.k * L.ci, n,
                                   c->grads + L.w_off, 0, S.s));
   return 0;
@@ -1152,6 +1102,8 @@ int build(seg_ctx* c) {
   c->n_moving = 2 * moff;
   c->n_stats = c->n_moving;
   {
+    // runtime knob (deliberate): the all-reduce bucket size, a property of the interconnect
+    // rather than of the kernels (seg_grad_buckets); results are identical for any value
     const char* e = getenv("SEG_BUCKET_MB");
     const long cap = (e ? std::max(1L, atol(e)) : 32L) * (1L << 20) / 4;   // floats per bucket
     long hi = c->n_decay;
@@ -1169,6 +1121,9 @@ int build(seg_ctx* c) {
     c->bk_ev.resize(c->bk_lo.size());
     for (auto& ev : c->bk_ev) HIPCALL(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     c->wg_done.assign(c->convs.size(), 0);
+    // runtime knob (deliberate): SEG_SIDE_STREAM=0 runs the backward on one stream, so a
+    // rocprofv3 trace sees kernel-alone durations (tools/session.sh stats, pmc_traffic.sh);
+    // results are bitwise identical either way
     const char* se = getenv("SEG_SIDE_STREAM");
     c->side_on = !(se && se[0] == '0');
     if (c->side_on) {
@@ -1343,35 +1298,8 @@ int build(seg_ctx* c) {
   }
   c->slab_floats = slab;
   if (int r = dalloc(c, &c->slab, slab)) return r;
-  {  // per-layer regions for the deferred reduces (side-stream split counts; not the stem's)
-    size_t tot = 0;
-    c->slab_off.assign(c->convs.size(), -1);
-    c->slab_cap.assign(c->convs.size(), 0);
-    for (size_t li = 0; li < c->convs.size(); ++li) {
-      if ((int)li == c->stem) continue;
-      const ConvL& L = c->convs[li];
-      const WgradArgs a = wgrad_problem(L, false);
-      const size_t per = (size_t)a.Co * a.KH * a.KW * a.C;
-      c->slab_off[li] = (long)tot;
-      c->slab_cap[li] = (long)(per * wgrad_splits(a, c->dt, true));
-      tot += (size_t)c->slab_cap[li];
-      tot = (tot + 63) / 64 * 64;   // 256-B aligned regions
-    }
-    // off by default: the batched reduce on the compute stream cost the step more than the
-    // per-layer reduces beside the chain (-0.8 %, profiles/r05_ab_defer_fold.txt)
-    const char* e = getenv("SEG_DEFER_REDUCE");
-    c->defer_red_on = e && e[0] == '1';
-    const char* f = getenv("SEG_BN_FOLD");
-    c->bq_on = f && f[0] == '1';
-    if (int r = dalloc(c, &c->slab_all, std::max<size_t>(c->defer_red_on ? tot : 0, 64))) return r;
-    if (int r = dalloc(c, &c->red_jobs, c->convs.size())) return r;
-  }
   if (int r = dalloc(c, &c->stat_scratch, std::max<size_t>(c->stat_scratch_floats, 16))) return r;
   {  // linear BN-backward fold: per-layer coefficients and the shared scratch (lbf.h)
-    const char* e = getenv("SEG_LBF");
-    c->lbf_on = !(e && e[0] == '0');
-    const char* el = getenv("SEG_LBF_LATE");
-    c->lbf_late = el && el[0] == '1';
     size_t wts = 0, hh = 0, hs = 0, ci_max = 0;
     for (auto& u : c->units) {
       if (!lbf_shape_ok(c, u)) continue;
@@ -1449,7 +1377,7 @@ const uint8_t* premask_bits(seg_ctx* c, const Unit* pred, int C) {
 // in_masked: u.dout arrived pre-masked (a projection unit folds only then: its gated gradient
 // is dout itself, and its dual BN reduce cannot store one)
 bool lbf_ok(seg_ctx* c, const Unit& u, bool in_masked) {
-  if (!c->lbf_on || c->bq_on || !c->lbf_wts || !lbf_shape_ok(c, u)) return false;
+  if (!c->lbf_on || !c->lbf_wts || !lbf_shape_ok(c, u)) return false;
   if (u.kind == SC_CONV) {
     const ConvL& L3 = c->convs[u.c3];
     const ConvL& Ls = c->convs[u.sc];
@@ -1570,8 +1498,7 @@ int lbf_backward(Step& S, Unit& u, const Act& dyhat) {
   p.coef = L.lbf_coef;
   HIPCALL(c, launch_lbf_prep(S.dt, p, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
-  if (!c->lbf_late)
-    if (int r = lbf_wgrad(S, u, dyhat)) return r;
+  if (int r = lbf_wgrad(S, u, dyhat)) return r;
   const double gbh = (2.0 * co * ci * c->esz + (double)ci * ci * (c->esz + 8.0 * lbf_hsplits(L))) * 1e-9;
   if (int r = prof_begin(c, S.s, 5, u.c3, gbh, &slot)) return r;
   WgradArgs h{};   // H[k][k'] = sum_c (D_c W3[c][k]) W3[c][k']: the channels c are the "pixels"
@@ -1595,8 +1522,6 @@ int lbf_backward(Step& S, Unit& u, const Act& dyhat) {
   if (ci > 128) HIPCALL(c, launch_conv_nt_pp(S.dt, a, S.s));
   else HIPCALL(c, launch_conv_nt_v2(S.dt, a, S.s));
   if (int r = prof_end(c, S.s, slot)) return r;
-  if (c->lbf_late)   // A/B: the weight gradient queued behind the data gradient
-    if (int r = lbf_wgrad(S, u, dyhat)) return r;
   L.lbf_done = true;
   L.lbf_dyhat = dyhat;
   ++c->lbf_launches;
@@ -1637,7 +1562,7 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred =
         if (int r = bn_backward(S, u.sc, u.dout, 0, &u.out, nullptr)) return r;
     }
     if (int r = conv_wgrad(S, u.c3, u.z2)) return r;
-    if (int r = conv_dgrad(S, u.c3, u.dz2, nullptr, nullptr, nullptr, u.c2, &u.z2)) return r;
+    if (int r = conv_dgrad(S, u.c3, u.dz2)) return r;
   }
   if (int r = bn_backward(S, u.c2, u.dz2, 0, &u.z2, nullptr, nullptr, lbf ? c->lbf_bias : nullptr, false,
                          lbf ? L3.lbf_cs : nullptr))
@@ -1645,7 +1570,7 @@ int unit_backward(Step& S, Unit& u, const Act& dx, bool accumulate, Unit* pred =
   if (lbf)
     if (int r = lbf_combine(S, u)) return r;
   if (int r = conv_wgrad(S, u.c2, u.z1)) return r;
-  if (int r = conv_dgrad(S, u.c2, u.dz1, nullptr, nullptr, nullptr, u.c1, &u.z1)) return r;
+  if (int r = conv_dgrad(S, u.c2, u.dz1)) return r;
   if (int r = bn_backward(S, u.c1, u.dz1, 0, &u.z1, nullptr)) return r;
   if (int r = conv_wgrad(S, u.c1, u.in)) return r;
   switch (u.kind) {
@@ -1803,16 +1728,8 @@ int backward(Step& S) {
   std::fill(c->wg_done.begin(), c->wg_done.end(), 0);
   c->bk_next = 0;
   // a profiled backward runs on one stream so the HIP-event kernel timings are kernel-alone
-  // a previous backward whose deferred reduces no update consumed: run them before the side
-  // stream (ordered after this point by ev_join) rewrites the slabs
-  if (int r = flush_reduces(c, S.s)) return r;
   c->side_active = c->side_on && !c->prof.on;
   c->prestem_rec = false;
-  // one process with a deferred stem: nothing reads the gradients before seg_apply_update, so
-  // every other layer's split-K reduce joins one batched launch there (not with loss scaling:
-  // seg_set_defer_stem is never set for fp16, and the overflow check reads the gradients)
-  c->defer_red = c->side_active && c->defer_stem && !c->skip_flag && c->slab_all && c->defer_red_on;
-  c->red_host.clear();
   if (c->side_active) {   // the side stream must not run ahead of the previous use of its buffers
     HIPCALL(c, hipEventRecord(c->ev_join, S.s));
     HIPCALL(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
@@ -1941,23 +1858,6 @@ int refresh_stem_pad(seg_ctx* c, hipStream_t s) {
 // on stream s reads or rewrites the step's buffers. The pending state is kept until the
 // gradient is consumed (seg_apply_update) or superseded (seg_backward): a join on another
 // stream must not let a later seg_apply_update skip its own join
-// the deferred split-K reduces of the step, on stream s (whose work already follows every
-// non-stem weight gradient: seg_backward's join on ev_prestem / ev_join)
-int flush_reduces(seg_ctx* c, hipStream_t s) {
-  if (!c->red_pending) return 0;
-  const int nj = (int)c->red_host.size();
-  // the table is the same every step (layers, regions, split counts): copied when it changes
-  if (c->red_dev.size() != c->red_host.size() ||
-      memcmp(c->red_dev.data(), c->red_host.data(), nj * sizeof(ReduceJob))) {
-    HIPCALL(c, hipStreamSynchronize(s));   // no launch of the previous table is still reading it
-    HIPCALL(c, hipMemcpy(c->red_jobs, c->red_host.data(), nj * sizeof(ReduceJob), hipMemcpyHostToDevice));
-    c->red_dev = c->red_host;
-  }
-  HIPCALL(c, launch_splitk_reduce_batched(c->red_jobs, nj, s));
-  c->red_pending = false;
-  return 0;
-}
-
 int join_stem(seg_ctx* c, hipStream_t s, bool consume = false) {
   if (!c->stem_pending) return 0;
   HIPCALL(c, hipStreamWaitEvent(s, c->ev_join, 0));
@@ -2201,7 +2101,6 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
                      st_hi <= c->n_decay;
   if (!split)
     if (int r = join_stem(c, s, true)) return r;
-  if (int r = flush_reduces(c, s)) return r;
   if (c->skip_flag) {   // loss-scaled (fp16) step: unscale, and skip it if anything overflowed
     HIPCALL(c, hipMemsetAsync(c->skip_flag, 0, sizeof(int), s));
     HIPCALL(c, launch_nonfinite(c->grads, c->n_train, c->skip_flag, s));
@@ -2270,10 +2169,8 @@ int seg_apply_update(seg_ctx* c, float lr, float momentum, float ema_decay_eff, 
 int seg_flush_grads(seg_ctx* c, void* stream) {
   NEED_BOUND(c);
   // a deferred stem weight gradient may still run on the weight-gradient stream: the caller's
-  // stream waits for it (without consuming the join seg_apply_update takes), then the deferred
-  // reduces run there
-  if (int r = join_stem(c, (hipStream_t)stream, false)) return r;
-  return flush_reduces(c, (hipStream_t)stream);
+  // stream waits for it (without consuming the join seg_apply_update takes)
+  return join_stem(c, (hipStream_t)stream, false);
 }
 
 int seg_set_defer_stem(seg_ctx* c, int on) {
@@ -2288,11 +2185,16 @@ int seg_set_premask(seg_ctx* c, int on) {
   return 0;
 }
 
+int seg_set_lbf(seg_ctx* c, int on) {
+  if (!c) return set_err(nullptr, -EINVAL, "null ctx");
+  c->lbf_on = on != 0;
+  return 0;
+}
+
 int seg_counter(seg_ctx* c, const char* name, int64_t* value) {
   if (!c || !name || !value) return set_err(c ? &c->err : nullptr, -EINVAL, "null argument");
   const std::string n(name);
   if (n == "premask_launches") *value = c->premask_launches;
-  else if (n == "bn_fold_launches") *value = c->bq_launches;
   else if (n == "lbf_layers") *value = c->lbf_launches;
   else return set_err(&c->err, -ENOENT, "unknown counter '%s'", name);
   return 0;

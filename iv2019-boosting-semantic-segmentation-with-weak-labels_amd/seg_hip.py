@@ -27,7 +27,8 @@ EXPORTED_SYMBOLS = [
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
     "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict", "seg_full_predictions",
-    "seg_set_nesterov", "seg_set_defer_stem", "seg_flush_grads", "seg_set_premask", "seg_counter",
+    "seg_set_nesterov", "seg_set_defer_stem", "seg_flush_grads", "seg_set_premask", "seg_set_lbf",
+    "seg_counter",
     "seg_crc32c", "seg_prepare_images", "seg_prepare_labels", "seg_prepare_images_crop",
 ]
 
@@ -122,6 +123,7 @@ def _load():
         "seg_set_defer_stem": (ip, [vp, ip]),
         "seg_flush_grads": (ip, [vp, vp]),
         "seg_set_premask": (ip, [vp, ip]),
+        "seg_set_lbf": (ip, [vp, ip]),
         "seg_counter": (ip, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     }
     override = "SEG_HIP_LIB" in os.environ   # A/B builds of older commits may lack new entries
@@ -231,7 +233,7 @@ class SegContext:
         """Host copies of named tensors of params/grads/momentum/ema."""
         buf = {"params": self.params, "grads": self.grads, "momentum": self.momentum,
                "ema": self.ema}[buffer]
-        if buffer == "grads":   # deferred split-K reduces (seg_set_defer_stem) run first
+        if buffer == "grads":   # a deferred stem weight gradient (seg_set_defer_stem) finishes first
             self.flush_grads()
         out = {}
         for p in self.param_info:
@@ -244,8 +246,8 @@ class SegContext:
         return out
 
     def flush_grads(self, stream=None):
-        """Run the step's deferred split-K reduces (seg_set_defer_stem) so the gradient buffer
-        is complete; a no-op otherwise."""
+        """Join a still-running deferred stem weight gradient (seg_set_defer_stem) on ``stream``
+        so the gradient buffer is complete; a no-op otherwise."""
         check(LIB.seg_flush_grads(self.h, _stream(stream)), self.h)
 
     # ---- step -----------------------------------------------------------------------
@@ -379,6 +381,11 @@ class SegContext:
     def set_premask(self, on):
         """seg_set_premask: pre-masked identity-unit gradients (default on; results unchanged)."""
         check(LIB.seg_set_premask(self.h, 1 if on else 0), self.h)
+
+    def set_lbf(self, on):
+        """seg_set_lbf: the linear BN-backward fold of the bottleneck conv3 layers (default on;
+        off = the separate BN-backward apply pass, the fold's reference path in tests)."""
+        check(LIB.seg_set_lbf(self.h, 1 if on else 0), self.h)
 
     def counter(self, name: str) -> int:
         """seg_counter: a runtime counter since creation (e.g. "premask_launches")."""

@@ -27,11 +27,12 @@ CASES = [
     (2, 16, 64, 64, 64, 3, 1, 1, False),      # one 64-channel chunk, Co 64
     (1, 24, 96, 128, 128, 3, 1, 1, False),    # two chunks (second patch streamed), Co 128
     (1, 8, 32, 128, 64, 3, 1, 1, False),      # two chunks, Co 64 (its dgrad: one chunk, Co 128)
-    # short-K dense 1x1, double-buffered accumulators (conv_db.hip: M % 256 == 0, Co % 128 == 0,
-    # 64 <= K <= 512); the dgrad of the same case is a short-K problem too where Ci > 128
-    (2, 16, 32, 256, 512, 1, 1, 1, False),    # K 256 -> 512: 4 x 4 tiles, one per workgroup
+    # short-K dense 1x1 on the persistent ping-pong loop (several tiles per workgroup: the next
+    # tile's prologue in flight during the epilogue); the dgrad of the same case is a short-K
+    # problem too where Ci > 128
+    (2, 16, 32, 256, 512, 1, 1, 1, False),    # K 256 -> 512: 4 x 2 tiles, one per workgroup
     (1, 16, 16, 64, 256, 1, 1, 1, False),     # K 64: one K-tile per tile
-    (1, 128, 128, 256, 1024, 1, 1, 1, False), # 512 tiles: two per workgroup (epilogue overlapped)
+    (1, 128, 128, 256, 1024, 1, 1, 1, False), # 256 tiles
     (1, 96, 128, 128, 768, 1, 1, 1, False),  # 288 tiles: 2 or 1 per workgroup, K 128
     (2, 64, 128, 512, 1024, 1, 1, 1, False),  # K 512, 512 tiles; its dgrad K 1024 (ping-pong)
 ]

@@ -208,16 +208,13 @@ def test_bf16_step_is_deterministic(cuda):
         assert np.array_equal(a["params"][k], b["params"][k]), k
 
 
-@pytest.mark.parametrize("dtype,defer_reduce", [("bf16", "0"), ("bf16", "1"), ("fp32", "1")])
-def test_defer_stem_update_matches(cuda, monkeypatch, dtype, defer_reduce):
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_defer_stem_update_matches(cuda, dtype):
     """seg_set_defer_stem (the update of every parameter but the stem's beside the stem's weight
-    gradient, then the stem's; every other layer's split-K reduce deferred to one batched launch
-    at the update): three steps with EMA give bitwise the same parameters, momentum and EMA
-    shadows as the joined update, and the last step's gradients (read between backward and
-    update through seg_flush_grads, which also joins the still-running stem weight gradient)
-    are bitwise the per-layer reduces'; the regulariser value (a sum in another order) 1e-6.
-    SEG_DEFER_REDUCE=1 (read at context creation) turns on the batched deferred reduces."""
-    monkeypatch.setenv("SEG_DEFER_REDUCE", defer_reduce)
+    gradient, then the stem's): three steps with EMA give bitwise the same parameters, momentum
+    and EMA shadows as the joined update, and the last step's gradients (read between backward
+    and update through seg_flush_grads, which joins the still-running stem weight gradient)
+    bitwise; the regulariser value (a sum in another order) 1e-6."""
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     cfg = SegConfig(height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp")
@@ -255,15 +252,14 @@ def test_defer_stem_update_matches(cuda, monkeypatch, dtype, defer_reduce):
 
 
 @pytest.mark.parametrize("dtype,depth", [("bf16", 50), ("fp16", 101)])
-def test_premask_matches(cuda, dtype, depth, monkeypatch):
+def test_premask_matches(cuda, dtype, depth):
     """seg_set_premask (identity units' conv1 data gradient, a projection unit's dual data
     gradient and decrease_fdims' store the previous unit's output gradient already ReLU-masked;
     that unit's c3 BN backward then reads it without the bits and writes no separate masked
     copy): three steps give bitwise the same losses, gradients, parameters and momentum as the
-    path that masks in the BN backward. With the linear BN-backward fold off (SEG_LBF=0): a
+    path that masks in the BN backward. With the linear BN-backward fold off (seg_set_lbf 0): a
     projection unit folds only when its gradient arrives pre-masked, so with the fold on the
     two arms would differ by the fold's own rounding (test_lbf_matches covers that)."""
-    monkeypatch.setenv("SEG_LBF", "0")
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     cfg = SegConfig(depth=depth, height=64, width=128, nb_pp=1, nb_pb=1, pyramid="aspp")
@@ -277,6 +273,7 @@ def test_premask_matches(cuda, dtype, depth, monkeypatch):
         ctx = SegContext(depth=depth, pyramid=cfg.pyramid, height=cfg.height, width=cfg.width,
                          nb_pp=1, nb_pb=1, dtype=dtype)
         ctx.load_params(params)
+        ctx.set_lbf(False)
         if dtype == "fp16":
             ctx.set_loss_scale(1024.0)
         ctx.set_premask(pm)
@@ -305,64 +302,14 @@ def test_premask_matches(cuda, dtype, depth, monkeypatch):
     assert np.array_equal(m0, m1)
 
 
-def test_bn_fold_matches(cuda, monkeypatch):
-    """SEG_BN_FOLD=1 (round 5): the BN-backward reduce of the units' conv1 /
-    conv2 BN layers folded into the epilogue of the data gradient that produces their output
-    gradient (one-tile ping-pong launches, Co > 128: the bottlenecks of blocks 3-4 and the three
-    adaptation bottlenecks). Against the unfolded step on the same inputs: everything the
-    backward computes before the first folded layers (the logits convs, the adaptation units'
-    conv3) bitwise equal; the first folded layers' gamma / beta gradients (each adaptation
-    unit's conv2 BN: the same dz and y, only the order of the fp32 partial sums differs) to
-    1e-5; their weight gradients (through the bf16 BN-backward output, where that order can move
-    a rounding) to 2e-2. Further down the bf16 chain a one-ulp change is amplified like any bf16
-    rounding at random init (test_bf16_layerwise's docstring), so those gradients are only
-    required finite."""
-    from input_pipelines.synthetic import batch
-    from seg_hip import SegContext
-    cfg = SegConfig(height=64, width=128, nb_pp=2, pyramid="aspp")
-    params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=13).items()}
-    data = batch(24, cfg.nb_pp, 0, 0, cfg.height, cfg.width)
-    img = torch.as_tensor(data["images"]).to(cuda)
-    px = torch.as_tensor(data["px"]).to(cuda)
-    out = []
-    for fold in ("0", "1"):
-        monkeypatch.setenv("SEG_BN_FOLD", fold)   # read at context creation
-        ctx = SegContext(pyramid=cfg.pyramid, height=cfg.height, width=cfg.width, nb_pp=2,
-                         dtype="bf16")
-        ctx.load_params(params)
-        ctx.forward(img)
-        ctx.loss(px, None, None)
-        ctx.backward()
-        torch.cuda.synchronize()
-        out.append((ctx.outputs()[0].cpu().numpy().copy(), ctx.named("grads")))
-        # the folded launches really ran (two per bottleneck with more than 128 middle
-        # channels: block3's 6, block4's 3, the 3 adaptation units) or really did not
-        n = ctx.counter("bn_fold_launches")
-        assert (n == 2 * (6 + 3 + 3)) if fold == "1" else (n == 0), (fold, n)
-        ctx.close()
-    (l0, g0), (l1, g1) = out
-    assert np.array_equal(l0, l1)   # the forward and the loss head are untouched
-    upstream = [k for k in g0 if k.startswith("softmax_classifier") or
-                (k.startswith("adaptation_module") and "/conv3/" in k)]
-    assert len(upstream) == 3 * 3 + 3 * 3
-    for k in upstream:
-        assert np.array_equal(g0[k], g1[k]), k
-    for head in ("l1", "l2_vehicle", "l2_human"):
-        a = f"adaptation_module/{head}_features/conv2/"
-        for t in ("gamma", "beta"):
-            assert _rel(g1[a + "BatchNorm/" + t], g0[a + "BatchNorm/" + t]) < 1e-5, (a, t)
-        assert _rel(g1[a + "weights"], g0[a + "weights"]) < 2e-2, a
-    assert all(np.all(np.isfinite(v)) for v in g1.values())
-
-
-def test_lbf_matches(cuda, monkeypatch):
+def test_lbf_matches(cuda):
     """Linear BN-backward fold (round 5, csrc/lbf.h): the conv3 BN-backward apply of the 16-bit
     bottlenecks with an expanding conv3 (every unit of R50's four blocks: the projection units
     through their pre-masked output gradient, their shortcut BN applied alone after the dual
     reduce; block1-2 data gradients on the v2 kernel's K-concatenated path) is
     replaced by the affine form dz3 = A dyhat + B + D z3 pushed through the data gradient
     ([dyhat | y2] x [A o W3 ; W3^T diag(D) W3], constant added by conv2's BN backward) and the
-    weight gradient (A o dyhat^T y2 + B colsum(y2) + D o W3 y2^T y2). Against SEG_LBF=0 on the
+    weight gradient (A o dyhat^T y2 + B colsum(y2) + D o W3 y2^T y2). Against seg_set_lbf(0) on the
     same inputs: the forward and loss bitwise, every gradient the backward computes before the
     first folded layer bitwise (the heads, the pyramid, decrease_fdims), the first folded
     layer's BN gamma / beta bitwise (its reduce is unchanged), its weight gradient and its conv2
@@ -378,10 +325,10 @@ def test_lbf_matches(cuda, monkeypatch):
     px = torch.as_tensor(data["px"]).to(cuda)
     out = []
     for on in ("0", "1"):
-        monkeypatch.setenv("SEG_LBF", on)   # read at context creation
         ctx = SegContext(pyramid=cfg.pyramid, height=cfg.height, width=cfg.width, nb_pp=2,
                          dtype="bf16")
         ctx.load_params(params)
+        ctx.set_lbf(on == "1")
         ctx.forward(img)
         ctx.loss(px, None, None)
         ctx.backward()
