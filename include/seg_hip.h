@@ -135,7 +135,10 @@ int seg_set_lbf(seg_ctx* ctx, int on);
  * "premask_launches" = data gradients stored pre-masked (seg_set_premask): identity units'
  *   conv1, and at block boundaries a projection unit's conv1 + shortcut and decrease_fdims';
  * "lbf_layers" = conv3 layers whose BN-backward apply was folded into their data / weight
- * gradients by linearity (seg_set_lbf). -ENOENT for an unknown name. */
+ * gradients by linearity (seg_set_lbf);
+ * "loss_yf_launches" = seg_loss calls whose loss head ran the y-first kernel (the full-res
+ *   columns of every block fit one 256-thread chunk: the 512 x 1024 and 1024 x 2048 shapes).
+ * -ENOENT for an unknown name. */
 int seg_counter(seg_ctx* ctx, const char* name, int64_t* value);
 
 /* outputs ------------------------------------------------------------------------------
@@ -242,8 +245,9 @@ int seg_bbox_labels(const float* boxes, const int32_t* cids, const int32_t* box_
 int seg_tag_labels(const float* tags, int n, int H, int W, float* out, void* stream);
 
 /* internal tensors for parity tests: "logits", "grad_un", "dzscale", "feat", "dfeat", "z0",
- * "head<h>_out", "head<h>_dout", "conv<i>_x" (input of the last forward), "conv<i>_y",
- * "conv<i>_dy" (i = creation index).
+ * "head<h>_out", "head<h>_dout", "pyr<b>_z" (pyramid branch b's BN + ReLU output at its pooled
+ * resolution), "conv<i>_x" (input of the last forward), "conv<i>_y", "conv<i>_dy" (i =
+ * creation index).
  * dims = N, H, W, C; ld = pixel stride; dtype = SEG_DTYPE_* of the storage */
 int seg_debug_tensor(seg_ctx* ctx, const char* name, void** ptr, int* dims, int* ld, int* dtype);
 

@@ -66,6 +66,8 @@ int loss_head_blocks(int N, int Hl, int Wl);
 hipError_t launch_eval_decisions(const EvalArgs& a, const LossTables& t, hipStream_t s);
 hipError_t launch_full_predictions(const FullPredArgs& a, const LossTables& t, hipStream_t s);
 hipError_t launch_loss_head(const LossArgs& a, const LossTables& t, hipStream_t s);
+// true when launch_loss_head takes the y-first kernel for this geometry (Cityscapes tables)
+bool loss_head_yf(int W, int Wl);
 // out[0..9] = {seg, l1, l2v, l2h, n1, n2v, n2h, f1, f2v, f2h}; dzscale[ldl] per-channel
 // factors (1/n1 | 0.1/n2v | 0.1/n2h; 0 where the count is 0)
 hipError_t launch_loss_finalize(const float* part, int nblocks, const LossTables& t, int ldl,

@@ -707,12 +707,16 @@ int loss_head_blocks(int N, int Hl, int Wl) {
   return N * ((Hl + LA - 1) / LA) * ((Wl + LB - 1) / LB);
 }
 
-hipError_t launch_loss_head(const LossArgs& a, const LossTables& t, hipStream_t s) {
-  dim3 g(loss_head_blocks(a.N, a.Hl, a.Wl));
+bool loss_head_yf(int W, int Wl) {
   // y-first accumulation when every block's full-resolution columns fit one chunk: (LB + 1)
   // low-res cells of (W - 1) / (Wl - 1) columns each, plus the two boundary columns
-  const double span = a.Wl > 1 ? (LB + 1) * (double)(a.W - 1) / (double)(a.Wl - 1) + 3.0 : 1e9;
-  const bool yf = LOSS_YF && span <= THREADS;
+  const double span = Wl > 1 ? (LB + 1) * (double)(W - 1) / (double)(Wl - 1) + 3.0 : 1e9;
+  return LOSS_YF && span <= THREADS;
+}
+
+hipError_t launch_loss_head(const LossArgs& a, const LossTables& t, hipStream_t s) {
+  dim3 g(loss_head_blocks(a.N, a.Hl, a.Wl));
+  const bool yf = loss_head_yf(a.W, a.Wl);
   if (t.c1 == 14 && t.c2 == 7 && t.c3 == 3 && yf)
     hipLaunchKernelGGL((loss_head_kernel<14, 7, 3, 1>), g, dim3(THREADS), 0, s, a, t);
   else if (t.c1 == 14 && t.c2 == 7 && t.c3 == 3)

@@ -212,6 +212,7 @@ struct seg_ctx {
   bool defer_stem = false;
   bool premask = true;             // seg_set_premask: pre-masked identity-unit gradients (unit_backward)
   int64_t premask_launches = 0;    // conv1 data gradients stored pre-masked (seg_counter)
+  int64_t loss_yf_launches = 0;    // loss heads run by the y-first kernel (seg_counter)
   bool prestem_rec = false;
   bool stem_pending = false;
   float* dzscale = nullptr;       // [ldl]
@@ -2015,6 +2016,7 @@ int seg_loss(seg_ctx* c, const int32_t* px, const float* bbox, const float* tag,
   a.grad_un = c->grad_un; a.part = c->loss_part; a.decisions = decisions;
   hipStream_t s = (hipStream_t)stream;
   HIPCALL(c, launch_loss_head(a, c->tables, s));
+  if (c->tables.c1 == 14 && loss_head_yf(a.W, a.Wl)) ++c->loss_yf_launches;
   HIPCALL(c, launch_loss_finalize(c->loss_part, c->loss_blocks, c->tables, c->ldl, c->loss_scale,
                                   c->loss_out, c->dzscale, s));
   return 0;
@@ -2196,6 +2198,7 @@ int seg_counter(seg_ctx* c, const char* name, int64_t* value) {
   const std::string n(name);
   if (n == "premask_launches") *value = c->premask_launches;
   else if (n == "lbf_layers") *value = c->lbf_launches;
+  else if (n == "loss_yf_launches") *value = c->loss_yf_launches;
   else return set_err(&c->err, -ENOENT, "unknown counter '%s'", name);
   return 0;
 }
@@ -2358,6 +2361,13 @@ int seg_debug_tensor(seg_ctx* c, const char* name, void** ptr, int* dims, int* l
       c->z0_stale = false;
     }
     a = c->z0;
+  }
+  else if (n.rfind("pyr", 0) == 0 && n.size() == 6 && n.substr(4) == "_z") {
+    // a pyramid branch's BN + ReLU output at its pooled resolution (PSP: grids 1, 2, 3, 6;
+    // ASPP: 0 = the image pool), the input of its align-corners resize into the concat
+    const int b = n[3] - '0';
+    if (b < 0 || b >= (int)c->zb.size() || !c->zb[b].p) return set_err(&c->err, -EINVAL, "bad pyramid branch");
+    a = c->zb[b];
   }
   else if (n.rfind("head", 0) == 0 && n.size() > 5) {
     int h = n[4] - '0';

@@ -214,25 +214,29 @@ def _maxpool_bwd(z0, g):
 # C4 = R101 + pyramid with the 1:2:1 strong : bbox : tag mix in bf16 (covers C3's kernels and
 # adds the weak-label loss head); C5 = the same mix in fp16 with fp32 master gradients under a
 # loss scale of 4096 (the dynamic scaler settles at 8192 on these weights)
+# C2-PSP = C2 with the reference's live pyramid module (_create_psp_module, hierarchical.py:
+# 186-207; the shipped checkpoint uses it, README.md:31): at 1024 x 2048 the 3- and 6-grids pool
+# 42 x 85 and 21 x 42 windows of the 128 x 256 map and drop the remainder rows and columns
 FULL_CONFIGS = [
-    ("C2", 50, "bf16", (4, 0, 0)),
-    ("C4", 101, "bf16", (1, 2, 1)),
-    ("C5", 101, "fp16", (1, 2, 1)),
+    ("C2", 50, "bf16", (4, 0, 0), "aspp"),
+    ("C2-PSP", 50, "bf16", (4, 0, 0), "psp"),
+    ("C4", 101, "bf16", (1, 2, 1), "aspp"),
+    ("C5", 101, "fp16", (1, 2, 1), "aspp"),
 ]
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("name,depth,dtype,mix", FULL_CONFIGS, ids=[c[0] for c in FULL_CONFIGS])
-def test_step_layerwise_fullsize(cuda, name, depth, dtype, mix):
+@pytest.mark.parametrize("name,depth,dtype,mix,pyramid", FULL_CONFIGS, ids=[c[0] for c in FULL_CONFIGS])
+def test_step_layerwise_fullsize(cuda, name, depth, dtype, mix, pyramid):
     from input_pipelines.synthetic import batch
     from seg_hip import SegContext
     H, W = 1024, 2048
     npp, npb, npi = mix
     NB = npp + npb + npi
-    cfg = SegConfig(depth=depth, height=H, width=W, nb_pp=npp, nb_pb=npb, nb_pi=npi, pyramid="aspp")
+    cfg = SegConfig(depth=depth, height=H, width=W, nb_pp=npp, nb_pb=npb, nb_pi=npi, pyramid=pyramid)
     params = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=2).items()}
     data = batch(17, npp, npb, npi, H, W)
-    ctx = SegContext(depth=depth, pyramid="aspp", height=H, width=W, nb_pp=npp, nb_pb=npb,
+    ctx = SegContext(depth=depth, pyramid=pyramid, height=H, width=W, nb_pp=npp, nb_pb=npb,
                      nb_pi=npi, dtype=dtype)
     ctx.load_params(params)
     if dtype == "fp16":
@@ -336,23 +340,63 @@ def test_step_layerwise_fullsize(cuda, name, depth, dtype, mix):
         out = X(il)
         g = unit_chain(f"adaptation_module/{h}_features", dgrad(il, out), out)
         dfeat = g if dfeat is None else dfeat + g
-    # ---- ASPP: final 1x1 over the 1280-channel concat, four conv branches, image pool
     pm = "feature_extractor/pyramid_module"
-    ifin = idx[f"{pm}/Conv_5"]
-    concat = X(ifin)
-    chk(ifin, dfeat, X(idx["adaptation_module/l1_features/conv1"]), "dfeat")
-    dconcat = dgrad(ifin, concat)
     fd = cfg.feature_dims_decreased
-    dz_dfd = 0
-    for b in range(1, 5):
-        ib = idx[f"{pm}/Conv_{b}"]
-        chk(ib, dconcat[..., b * fd:(b + 1) * fd], concat[..., b * fd:(b + 1) * fd], "ASPP concat")
-        dz_dfd = dz_dfd + dgrad(ib, X(ib))
-    ip = idx[f"{pm}/Conv"]
-    chk(ip, dconcat[..., :fd].sum((1, 2), keepdim=True), concat[:, :1, :1, :fd], "ASPP image pool")
-    dz_dfd = dz_dfd + dgrad(ip, X(ip)) / (X(ifin).shape[1] * X(ifin).shape[2])
     idfd = idx["feature_extractor/extension/decrease_fdims"]
-    chk(idfd, dz_dfd, X(idx[f"{pm}/Conv_1"]), "ASPP inputs")
+    if pyramid == "aspp":
+        # ---- ASPP: final 1x1 over the 1280-channel concat, four conv branches, image pool
+        ifin = idx[f"{pm}/Conv_5"]
+        concat = X(ifin)
+        chk(ifin, dfeat, X(idx["adaptation_module/l1_features/conv1"]), "dfeat")
+        dconcat = dgrad(ifin, concat)
+        dz_dfd = 0
+        for b in range(1, 5):
+            ib = idx[f"{pm}/Conv_{b}"]
+            chk(ib, dconcat[..., b * fd:(b + 1) * fd], concat[..., b * fd:(b + 1) * fd], "ASPP concat")
+            dz_dfd = dz_dfd + dgrad(ib, X(ib))
+        ip = idx[f"{pm}/Conv"]
+        chk(ip, dconcat[..., :fd].sum((1, 2), keepdim=True), concat[:, :1, :1, :fd], "ASPP image pool")
+        dz_dfd = dz_dfd + dgrad(ip, X(ip)) / (X(ifin).shape[1] * X(ifin).shape[2])
+        chk(idfd, dz_dfd, X(idx[f"{pm}/Conv_1"]), "ASPP inputs")
+    else:
+        # ---- PSP (hierarchical.py:186-207): concat = [z | resize(relu(bn(conv(avgpool_k(z)))))
+        # for the grids k = 1, 2, 3, 6], the 1280 -> 256 Conv_4 over it. Forward: the pooled
+        # inputs (VALID windows of (hf/8, wf/8) // k, remainder rows / columns dropped) and the
+        # align-corners resizes into the concat; backward: the resize transposes, the branch BN
+        # backward gated by the branch's own ReLU output, the branch data gradients and the
+        # average-pool transposes summed with the identity slice into decrease_fdims' output
+        # gradient. float64 references; pooling and resizing by torch on the device
+        import torch.nn.functional as F
+        from oracle.tfseg import psp_grids
+        ifin = idx[f"{pm}/Conv_4"]
+        concat = X(ifin)
+        z = concat[..., :fd].permute(0, 3, 1, 2)                       # NCHW, decrease_fdims output
+        hf, wf = z.shape[2], z.shape[3]
+        chk(ifin, dfeat, X(idx["adaptation_module/l1_features/conv1"]), "dfeat")
+        dconcat = dgrad(ifin, concat)
+        dz_dfd = dconcat[..., :fd].clone()
+        grids = psp_grids(H, W)
+        assert grids[2] == (42, 85) and grids[3] == (21, 42)          # the dropped remainders
+        for b, nm in enumerate(["Conv", "Conv_1", "Conv_2", "Conv_3"]):
+            ib = idx[f"{pm}/{nm}"]
+            kh, kw = grids[b]
+            pooled = F.avg_pool2d(z, (kh, kw), stride=(kh, kw)).permute(0, 2, 3, 1)
+            _elementwise(X(ib), pooled, 2 * u, 1e-3, f"PSP pool {nm} ({kh}x{kw})")
+            zb = ctx.debug_device(f"pyr{b}_z").double()
+            up = F.interpolate(zb.permute(0, 3, 1, 2), size=(hf, wf), mode="bilinear",
+                               align_corners=True).permute(0, 2, 3, 1)
+            _elementwise(concat[..., (b + 1) * fd:(b + 2) * fd], up, 2 * u, 1e-3, f"PSP resize {nm}")
+            src = torch.zeros_like(zb.permute(0, 3, 1, 2), requires_grad=True)
+            F.interpolate(src, size=(hf, wf), mode="bilinear", align_corners=True).backward(
+                dconcat[..., (b + 1) * fd:(b + 2) * fd].permute(0, 3, 1, 2))
+            dzb = src.grad.permute(0, 2, 3, 1)
+            chk(ib, dzb, zb, f"PSP resize transpose {nm}")
+            dpool = dgrad(ib, X(ib))
+            zin = torch.zeros_like(z, requires_grad=True)
+            F.avg_pool2d(zin, (kh, kw), stride=(kh, kw)).backward(dpool.permute(0, 3, 1, 2))
+            dz_dfd += zin.grad.permute(0, 2, 3, 1)
+            del zb, up, src, dzb, dpool, zin
+        chk(idfd, dz_dfd, concat[..., :fd], "PSP inputs")
     # ---- encoder units, top down, through residual / subsample / projection shortcuts
     rn = f"feature_extractor/base/resnet_v1_{depth}"
     scopes = [f"{rn}/{unit[0]}" for unit in resnet_units(depth, 8)]

@@ -671,9 +671,15 @@ def test_frozen_bn_train_step_fp32(cuda):
 # hierarchical.py:143-184). Nothing upstream of the logits enters, so this is well conditioned
 # (unlike the parameter gradients above) and held at 1e-5 per head (measured 0.6-1.7e-7 on one
 # box, profiles/r04_loss_grad.txt).
+# the first three take the per-row loss-head kernel; 64 x 512 (low-res 8 x 64, ragged 30-column
+# blocks) takes the y-first kernel the production shapes run (loss_head_yf), 64 x 1024
+# too with a weak mix
 LOSS_GRAD = [SegConfig(height=48, width=64, nb_pp=1, nb_pb=1, pyramid="none"),
              SegConfig(height=64, width=96, nb_pp=1, nb_pb=1, nb_pi=1, pyramid="psp"),
-             SegConfig(height=64, width=128, nb_pp=2, pyramid="aspp")]
+             SegConfig(height=64, width=128, nb_pp=2, pyramid="aspp"),
+             SegConfig(height=64, width=512, nb_pp=1, nb_pb=1, pyramid="none"),
+             SegConfig(height=48, width=1024, nb_pp=1, nb_pb=1, nb_pi=1, pyramid="none")]
+YF_SHAPES = {(64, 512), (48, 1024)}
 
 
 @pytest.mark.parametrize("cfg", LOSS_GRAD, ids=lambda c: f"{c.height}x{c.width}-{c.nb_pp}{c.nb_pb}{c.nb_pi}-{c.pyramid}")
@@ -692,6 +698,8 @@ def test_loss_head_gradient_fp32(cuda, cfg):
     tg = torch.as_tensor(data["tag"]).to(cuda) if cfg.nb_pi else None
     ctx.forward(img)
     ctx.loss(px, bb, tg)
+    # which loss-head kernel ran (y-first for the wide shapes, as at 512 x 1024 / 1024 x 2048)
+    assert ctx.counter("loss_yf_launches") == (1 if (cfg.height, cfg.width) in YF_SHAPES else 0)
     hd = torch.empty((cfg.nb, cfg.height, cfg.width, 3), dtype=torch.int32, device=cuda)
     ctx.full_predictions(head_decisions=hd)
     losses, _, logits = ctx.outputs()
