@@ -214,65 +214,31 @@ def train_py_leg(args, steps=10, warmup=3):
 
 def launch_ranks(n, argv):
     """`bench.py --gpus N` without WORLD_SIZE: start N child processes of this script (never an
-    exec of this one), rank r on GPU r, rendezvous on 127.0.0.1. Runs before anything in this
-    process touches the GPU. Returns the exit code: 0 only if every rank exited 0 and rank 0
-    printed the JSON line (re-printed here on stdout). A failing rank stops the others."""
-    import signal
-    import socket
-    import subprocess
-    import tempfile
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    tmp = tempfile.mkdtemp(prefix="seg_bench_ranks_")
-    procs, outs = [], []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        out = open(os.path.join(tmp, f"rank{r}.out"), "w+")
-        outs.append(out)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
-                                      env=env, stdout=out, start_new_session=True))
-    rc = 0
-    try:
-        live = set(range(n))
-        while live:
-            for r in sorted(live):
-                c = procs[r].poll()
-                if c is None:
-                    continue
-                live.discard(r)
-                if c != 0:
-                    print(f"bench.py: rank {r} exited with {c}; stopping the other ranks",
-                          file=sys.stderr, flush=True)
-                    rc = rc or (c if c > 0 else 1)
-            if rc:
-                break
-            time.sleep(0.2)
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                try:
-                    os.killpg(p.pid, signal.SIGTERM)
-                except OSError:
-                    pass
-        for p in procs:
-            try:
-                p.wait(timeout=30)
-            except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
-                p.wait()
-    line = None
-    for r, out in enumerate(outs):
-        out.seek(0)
-        for ln in out.read().splitlines():
-            if r == 0 and ln.startswith('{"metric"'):
-                line = ln
-            else:
-                print(f"[rank {r}] {ln}", file=sys.stderr)
-        out.close()
+    exec of this one; utils/launch.spawn_ranks: rank r on GPU r, rendezvous on 127.0.0.1, the
+    children in this process group, SIGTERM / SIGINT forwarded, a wall-clock deadline). Runs
+    before anything in this process touches the GPU. Returns the exit code: 0 only if every
+    rank exited 0 and rank 0 printed the JSON line (re-printed here on stdout). A failing rank
+    stops the others."""
     import shutil
-    shutil.rmtree(tmp, ignore_errors=True)
+    import tempfile
+    from utils.launch import spawn_ranks
+    tmp = tempfile.mkdtemp(prefix="seg_bench_ranks_")
+    outs = [open(os.path.join(tmp, f"rank{r}.out"), "w+") for r in range(n)]
+    try:
+        rc = spawn_ranks(n, [sys.executable, os.path.abspath(__file__)] + argv, outs=outs,
+                         deadline_s=float(os.environ.get("SEG_BENCH_DEADLINE_S", "1800")), name="bench.py")
+        line = None
+        for r, out in enumerate(outs):
+            out.seek(0)
+            for ln in out.read().splitlines():
+                if r == 0 and ln.startswith('{"metric"'):
+                    line = ln
+                else:
+                    print(f"[rank {r}] {ln}", file=sys.stderr)
+    finally:
+        for out in outs:
+            out.close()
+        shutil.rmtree(tmp, ignore_errors=True)
     if rc == 0 and line is None:
         print("bench.py: rank 0 printed no result line", file=sys.stderr)
         rc = 1
@@ -318,11 +284,9 @@ def main():
     backend = os.environ.get("SEG_BENCH_BACKEND", "nccl")
     # one rank per GPU (the driver's launch); more ranks than GPUs only for the one-GPU
     # rehearsal of the N > 1 path (SEG_BENCH_BACKEND=gloo: RCCL does not share a device)
+    from utils.launch import rank_device
     ndev = torch.cuda.device_count()
-    if local >= ndev and backend == "nccl":
-        raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} visible GPU(s): one rank per GPU "
-                           "(SEG_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs)")
-    local_dev = local % ndev if ndev else local
+    local_dev = rank_device(local, backend, ndev)
     shared_device = world > max(ndev, 1)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)

@@ -4,7 +4,8 @@ Same constructor ``SemanticSegmentation(input_fns, model_fn, settings)``, same s
 post-processing (problem definition, ``output_Nclasses``, learning-rate boundaries in
 epochs -> steps, defaults and validation), ``.train()`` runs the step loop on the native
 path. Data parallelism is one process per GPU (``torch.distributed``, backend 'nccl' =
-RCCL): launch with ``torchrun`` and pass ``--distribute``. ``.predict()``/``.evaluate()``
+RCCL): ``train.py ... --distribute`` starts one rank per visible GPU itself (or runs as one
+rank of an external ``torchrun`` launch). ``.predict()``/``.evaluate()``
 (inference, visualisation, eval with moving-statistics BN) are out of scope.
 
 Checkpoints are ``<log_dir>/model.ckpt-<step>.pt`` state dicts (named parameters, momentum,
@@ -110,10 +111,15 @@ class SemanticSegmentation(object):
         s = self._settings
         self._prepare_train_settings()
         if s.distribute:
+            # one process per GPU (train.main starts them when no launcher did, utils/launch.py);
+            # SEG_TRAIN_BACKEND=gloo rehearses N ranks on fewer GPUs (RCCL cannot share one)
             import torch.distributed as dist
+            from utils.launch import rank_device
+            backend = os.environ.get('SEG_TRAIN_BACKEND', 'nccl' if torch.cuda.is_available() else 'gloo')
+            torch.cuda.set_device(rank_device(int(os.environ.get('LOCAL_RANK', 0)), backend,
+                                              torch.cuda.device_count()))
             if not dist.is_initialized():
-                dist.init_process_group(backend='nccl' if torch.cuda.is_available() else 'gloo')
-            torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', 0)))
+                dist.init_process_group(backend=backend)
         rank = int(os.environ.get('RANK', 0))
         os.makedirs(s.log_dir, exist_ok=True)
         if rank == 0:
@@ -149,9 +155,11 @@ class SemanticSegmentation(object):
             spec = self._estimator_fn(ModeKeys.TRAIN, features, labels, config=config, params=s)
             ctx = spec.predictions['_context']
             losses = spec.train_op()
-            if rank == 0 and (step.value % s.save_summaries_steps == 0 or step.value == total):
+            # every rank logs its own loss terms (rank r > 0 tagged: under train.py's own
+            # launch its stdout is <log_dir>/rank<r>.log)
+            if step.value % s.save_summaries_steps == 0 or step.value == total:
                 torch.cuda.synchronize()
-                log_fn(f"step {step.value}: total {float(losses['total']):.4f} "
+                log_fn(f"{f'[rank {rank}] ' if rank else ''}step {step.value}: total {float(losses['total']):.4f} "
                        f"l1 {float(losses['l1_segmentation']):.4f} "
                        f"l2v {float(losses['l2_vehicle_segmentation']):.4f} "
                        f"l2h {float(losses['l2_human_segmentation']):.4f} "

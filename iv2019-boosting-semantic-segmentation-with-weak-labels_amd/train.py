@@ -10,7 +10,13 @@ TFRecord path the real-data input runs (host decode, device preprocessing and de
 rasterisation, input_pipelines/train_inputs.heterogeneous_train_input); without one, the
 train input_fn yields seeded synthetic batches in the same input contract
 (per_pixel_per_bbox_per_image.py:50-77).
-Multi-GPU: ``torchrun --nproc-per-node N train.py ... --distribute`` (one process per GPU).
+Multi-GPU: ``python train.py ... --distribute`` takes every visible GPU in one launch, as the
+reference's MirroredStrategy does (system_factory.py:276-283): without WORLD_SIZE in the
+environment, main() starts one rank process per GPU (utils/launch.spawn_ranks; rank 0 keeps the
+console log, the settings file and the checkpoints, rank r > 0 logs to <log_dir>/rank<r>.log)
+and fails if any rank fails. Under an external launcher (``torchrun --nproc-per-node N``)
+WORLD_SIZE is set and the process is one rank. ``SEG_TRAIN_RANKS`` overrides the rank count
+and ``SEG_TRAIN_BACKEND=gloo`` lets them share fewer GPUs (tests on one GPU).
 """
 import os
 import sys
@@ -133,8 +139,34 @@ def build_system(argv):
     return SemanticSegmentation({'train': train_input_fn(settings)}, model_fn, settings), settings
 
 
+def launch_distributed(argv, settings):
+    """`--distribute` without a launcher: one rank process of this script per visible GPU
+    (module docstring). Returns 0 when every rank finished; raises if any failed."""
+    from utils.launch import spawn_ranks, visible_gpus
+    n = int(os.environ.get('SEG_TRAIN_RANKS', 0)) or visible_gpus()
+    if n < 1:
+        raise RuntimeError('--distribute: no visible GPU')
+    os.makedirs(settings.log_dir, exist_ok=True)
+    logs = [None] + [open(os.path.join(settings.log_dir, f'rank{r}.log'), 'w') for r in range(1, n)]
+    try:
+        rc = spawn_ranks(n, [sys.executable, '-u', os.path.abspath(__file__)] + list(argv),
+                         outs=logs, name='train.py --distribute')
+    finally:
+        for f in logs[1:]:
+            f.close()
+    if rc != 0:
+        raise RuntimeError(f'train.py --distribute: a rank failed (exit {rc}); rank logs in '
+                           f'{settings.log_dir}/rank<r>.log')
+    return 0
+
+
 def main(argv):
+    """Trains on this process (one rank, or the whole run without --distribute) and returns
+    the number of steps run; with --distribute and no launcher it starts the ranks itself and
+    returns 0 once all of them finished."""
     system, settings = build_system(argv)
+    if settings.distribute and 'WORLD_SIZE' not in os.environ:
+        return launch_distributed(argv, settings)
     return system.train(max_steps=settings.max_steps)
 
 

@@ -248,9 +248,6 @@ def test_four_ranks_mixed_batch_matches_oracle(tmp_path):
     cfg = SegConfig(height=DP4_H, width=DP4_W, nb_pp=1, nb_pb=2, nb_pi=1, pyramid="none")
     p0 = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=0).items()}
 
-    from tests.test_gpu_train import _gate_flips
-    flips = []
-
     from test_gpu_train import _gate_flips   # tests/ is on sys.path (pytest's prepend mode)
     flips = []
 
@@ -282,9 +279,6 @@ def test_four_ranks_mixed_batch_matches_oracle(tmp_path):
     for r in range(DP4_WORLD):
         np.testing.assert_allclose(res[r][1][0][1], ref_l[r], rtol=1e-3, atol=1e-6, err_msg=f"rank {r}")
         assert tuple(res[r][1][0][2]) == ref_c[r], (r, res[r][1][0][2], ref_c[r])
-    # the weak-weight gate itself (as test_gpu_train): the oracle's own l1 argmax moves at most
-    # 0.1 % of a weak image's pixels in or out of a head's weights on every rank
-    assert all(int(f.max()) <= max(2, DP4_H * DP4_W // 1000) for f in flips), flips
     # the weak-weight gate itself (as test_gpu_train): the oracle's own l1 argmax moves at most
     # 0.1 % of a weak image's pixels in or out of a head's weights on every rank
     assert len(flips) == DP4_WORLD
@@ -328,3 +322,78 @@ def _moving_offsets(cfg):
            if p.kind in ("moving_mean", "moving_variance")}
     ctx.close()
     return out
+
+
+def test_train_distribute_launches_its_own_ranks(tmp_path):
+    """`train.py ... --distribute` with no launcher starts its ranks itself
+    (utils/launch.spawn_ranks, as the reference's MirroredStrategy takes every visible GPU in one
+    launch, system_factory.py:276-283). Two ranks share this box's one GPU over gloo
+    (SEG_TRAIN_RANKS=2, SEG_TRAIN_BACKEND=gloo; one card cannot host two RCCL ranks), one fp32
+    step at 64 x 128 with the global batch of 4 per-pixel images (2 per rank). Checked: the run
+    exits 0; rank 0's console log and rank 1's <log_dir>/rank1.log carry each rank's own loss
+    terms, equal to the oracle on that rank's shard (train.synthetic_train_input's seeds) at
+    1e-3 (4-decimal log values); rank 0's checkpoint holds the mean of the two ranks' updates
+    (step 0 of MomentumOptimizer and the BN moving averages are linear in the gradient and the
+    batch statistics, so the expected state is the mean of the per-rank oracle updates) at
+    max(1e-2, 3 x the fp32 oracle's gap) for the parameter change and max(1e-3, 4 x) for the
+    moving statistics. A failing rank fails the run: test_host.py covers that on the CPU."""
+    import re
+    import subprocess
+    import sys
+    import torch
+    from input_pipelines.synthetic import batch
+    from oracle.tfseg import OracleNet, SegConfig, init_params
+    H, W, NPP, LR = 64, 128, 4, 1e-3
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    train_py = os.path.join(repo, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd", "train.py")
+    log_dir = str(tmp_path / "logs")
+    env = dict(os.environ, SEG_TRAIN_RANKS="2", SEG_TRAIN_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, train_py, log_dir, "cityscapes", "--max_steps", "1",
+                        "--compute_dtype", "fp32", "--height_feature_extractor", str(H),
+                        "--width_feature_extractor", str(W), "--Nb_per_pixel", str(NPP),
+                        "--Nb_per_bbox", "0", "--Nb_per_image", "0", "--learning_rate_initial", str(LR),
+                        "--save_summaries_steps", "1", "--save_checkpoints_steps", "100", "--distribute"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    pat = r"step 1: total ([-\d.]+) l1 ([-\d.]+) l2v ([-\d.]+) l2h ([-\d.]+)"
+    logs = [r.stdout, open(os.path.join(log_dir, "rank1.log")).read()]
+    assert "training 1 steps on 2 GPU(s)" in r.stdout, r.stdout
+    got = [np.array([float(v) for v in re.findall(pat, t)[0]]) for t in logs]
+    state = torch.load(os.path.join(log_dir, "model.ckpt-1.pt"), weights_only=True)
+    assert state["global_step"] == 1 and "ema" not in state   # --distribute drops the EMA
+    nat = {k: v.numpy() for k, v in state["params"].items()}
+
+    cfg = SegConfig(height=H, width=W, nb_pp=NPP // 2, pyramid="none")
+    p0 = {k: v.astype(np.float32) for k, v in init_params(cfg, seed=0).items()}
+
+    def oracle(dtype):
+        losses, news = [], []
+        for rank in range(2):
+            d = batch(1000003 * rank, NPP // 2, 0, 0, H, W)   # train.synthetic_seed(rank, 0)
+            net = OracleNet(cfg, {k: v.astype(np.float64) for k, v in p0.items()}, dtype=dtype)
+            L, _, _, new_p, _, _, _ = net.train_step(d["images"], d["px"], lr=LR)
+            losses.append(np.array([float(L[n]) for n in ("total", "l1_segmentation",
+                                                           "l2_vehicle_segmentation", "l2_human_segmentation")]))
+            news.append({k: v.detach().numpy() for k, v in new_p.items()})
+        return losses, {k: (news[0][k] + news[1][k]) / 2 for k in news[0]}
+
+    ref_l, ref_p = oracle(torch.float64)
+    _, p32 = oracle(torch.float32)
+    for rank in range(2):
+        np.testing.assert_allclose(got[rank], ref_l[rank], rtol=1e-3, atol=1e-4, err_msg=f"rank {rank}")
+    assert not np.allclose(ref_l[0], ref_l[1])   # the ranks trained on different shards
+
+    def rel(a, b):
+        return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+    trained = sorted(k for k in ref_p if "moving" not in k)
+    moving = sorted(k for k in ref_p if "moving" in k)
+    flat = lambda d, ks: np.concatenate([np.asarray(d[k], np.float64).reshape(-1) for k in ks])
+    w0 = flat(p0, trained)
+    err = rel(flat(nat, trained) - w0, flat(ref_p, trained) - w0)
+    gap = rel(flat(p32, trained) - w0, flat(ref_p, trained) - w0)
+    assert err < max(1e-2, 3 * gap), (err, gap)
+    err_m = rel(flat(nat, moving), flat(ref_p, moving))
+    gap_m = rel(flat(p32, moving), flat(ref_p, moving))
+    assert err_m < max(1e-3, 4 * gap_m), (err_m, gap_m)

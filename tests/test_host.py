@@ -277,3 +277,107 @@ def test_bench_launches_ranks_and_propagates_failure():
     assert "exited with" in r.stderr, r.stderr[-2000:]
     # each child saw its own rank environment (whichever rank failed first is reported)
     assert "LOCAL_RANK" in r.stderr and ("rank 0" in r.stderr or "rank 1" in r.stderr)
+
+
+# ---- utils/launch.py: the self-launch of `bench.py --gpus N` and `train.py --distribute` ----
+_RANK_SCRIPT = """
+import os, sys, time
+out = sys.argv[1]
+r = int(os.environ["RANK"])
+with open(os.path.join(out, f"r{r}.txt"), "w") as f:
+    f.write(" ".join(os.environ[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
+                                               "MASTER_ADDR", "MASTER_PORT")) + " " + str(os.getpid()))
+mode = sys.argv[2]
+if mode == "fail1" and r == 1:
+    sys.exit(3)
+if mode in ("fail1", "sleep"):
+    time.sleep(60)
+"""
+
+
+def _rank_script(tmp_path):
+    p = tmp_path / "rank.py"
+    p.write_text(_RANK_SCRIPT)
+    return str(p)
+
+
+def test_spawn_ranks_sets_rank_environment(tmp_path):
+    import sys
+    from utils.launch import spawn_ranks
+    rc = spawn_ranks(3, [sys.executable, _rank_script(tmp_path), str(tmp_path), "ok"])
+    assert rc == 0
+    rows = [(tmp_path / f"r{r}.txt").read_text().split() for r in range(3)]
+    assert [row[:5] for row in rows] == [[str(r), str(r), "3", "3", "127.0.0.1"] for r in range(3)]
+    assert len({row[5] for row in rows}) == 1   # one rendezvous port
+
+
+def test_spawn_ranks_failure_stops_the_others(tmp_path):
+    import sys
+    import time
+    from utils.launch import spawn_ranks
+    t0 = time.monotonic()
+    rc = spawn_ranks(2, [sys.executable, _rank_script(tmp_path), str(tmp_path), "fail1"])
+    assert rc == 3 and time.monotonic() - t0 < 30   # rank 0 (sleeping 60 s) was stopped
+
+
+def test_spawn_ranks_deadline(tmp_path):
+    import sys
+    import time
+    from utils.launch import spawn_ranks
+    t0 = time.monotonic()
+    rc = spawn_ranks(2, [sys.executable, _rank_script(tmp_path), str(tmp_path), "sleep"], deadline_s=1.0)
+    assert rc == 124 and time.monotonic() - t0 < 30
+
+
+def test_spawn_ranks_forwards_sigterm(tmp_path):
+    """a signal to the launching process (e.g. `timeout` ending bench.py --gpus N)
+    reaches every rank; the parent exits 128 + SIGTERM and no rank is left running."""
+    import signal
+    import subprocess
+    import sys
+    import time
+    parent = tmp_path / "parent.py"
+    parent.write_text(
+        "import sys\n"
+        f"sys.path.insert(0, {os.path.join(REPO, 'iv2019-boosting-semantic-segmentation-with-weak-labels_amd')!r})\n"
+        "from utils.launch import spawn_ranks\n"
+        f"sys.exit(spawn_ranks(2, [sys.executable, {_rank_script(tmp_path)!r}, {str(tmp_path)!r}, 'sleep']))\n")
+    p = subprocess.Popen([sys.executable, str(parent)])
+    for _ in range(200):
+        if all((tmp_path / f"r{r}.txt").exists() for r in range(2)):
+            break
+        time.sleep(0.1)
+    time.sleep(0.3)
+    pids = [int((tmp_path / f"r{r}.txt").read_text().split()[-1]) for r in range(2)]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=40) == 128 + signal.SIGTERM
+    for pid in pids:
+        alive = True
+        for _ in range(50):
+            try:
+                os.kill(pid, 0)
+                with open(f"/proc/{pid}/stat") as f:
+                    if f.read().split()[2] == "Z":
+                        alive = False
+                        break
+            except (ProcessLookupError, FileNotFoundError):
+                alive = False
+                break
+            time.sleep(0.1)
+        assert not alive, pid
+
+
+def test_train_distribute_self_launch_propagates_failure(tmp_path):
+    """`train.py --distribute` without WORLD_SIZE starts its ranks itself (SEG_TRAIN_RANKS=2
+    here); with no GPU both fail at device selection, and the launch must fail, naming the
+    failing rank, instead of hanging or exiting 0."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(SEG_TRAIN_RANKS="2")
+    train_py = os.path.join(REPO, "iv2019-boosting-semantic-segmentation-with-weak-labels_amd", "train.py")
+    r = subprocess.run([sys.executable, train_py, str(tmp_path / "logs"), "cityscapes", "--max_steps", "1",
+                        "--distribute"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "exited with" in r.stderr and "a rank failed" in r.stderr, r.stderr[-3000:]
