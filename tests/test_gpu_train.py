@@ -449,15 +449,28 @@ def test_train_main_c1_reference_default_shape(cuda, tmp_path, monkeypatch):
 
 
 @pytest.mark.timeout(900)
-def test_train_main_c1_trajectory_bare_tolerance(cuda, tmp_path, monkeypatch, capsys):
+def test_train_main_c1_trajectory_needs_the_fp32_gap(cuda, tmp_path, monkeypatch, capsys):
     """is the relaxed trajectory bound of the 64 x 128 tests (steps 1-2 at
     max(1e-3, 3 x the fp32 oracle's own gap)) needed at a realistic shape? Three chained
     ``train.main`` steps at BASELINE config C1 (R50, no pyramid, 512 x 1024, 2 per-pixel images,
     fp32, the default learning rate 0.01, EMA 0.9; train.synthetic_train_input's batches 0-2 on
     rank 0) against OracleNet.train_step chained in float64 from the same initialisation (the
-    oracle fed its own previous parameters, momentum and EMA shadows): all four device-read loss
-    terms held at a BARE rtol 1e-3 on every step, the non-zero-weight counts exact. The float32
-    oracle chain is run beside it only to report its own gap (printed, not used as a bound)."""
+    oracle fed its own previous parameters, momentum and EMA shadows), and the same chain in
+    float32 beside it.
+
+    Answer (first run, profiles/r06_c1_trajectory.txt): yes. At lr 0.01 the float32 ORACLE
+    itself is 0.4-1.3e-2 off float64 on the step-1 / step-2 loss terms (l2 heads worst), while
+    step 0 agrees to 2e-6; the parameter change w3 - w0 differs by 0.67 (L2-relative) for the
+    float32 oracle and the native chain alike. The native chain tracks float64 as closely as the
+    float32 restatement does (per term at most 1.3x its gap; 0.26-1.0x on 7 of the 8). So no
+    fp32 implementation meets a bare 1e-3 after the first update at this learning rate; the
+    1.30e-3 vs 6.5e-4 of the 64 x 128 run is that same fp32 divergence, not a native defect.
+
+    Asserted: step 0 at a bare rtol 1e-3 on all four device-read loss terms, counts exact every
+    step; steps 1-2 per term at max(1e-3, 2 x the float32 oracle's own gap) (tighter than the
+    small tests' 3x); the float32 oracle's own gap above 1e-3 on some step-1/2 term (the fact
+    that makes the bare bound unreachable); the parameter change and momentum within 1.5x the
+    float32 oracle's own distance from float64."""
     import train
     from estimator.define_estimator_hierarchical import get_or_create_global_step
     from input_pipelines.synthetic import batch
@@ -509,14 +522,16 @@ def test_train_main_c1_trajectory_bare_tolerance(cuda, tmp_path, monkeypatch, ca
     ref = np.array(ref_l)
     err = np.abs(got - ref) / np.abs(ref)
     gap32 = np.abs(np.array(l32) - ref) / np.abs(ref)
-    print("C1 trajectory: native rel err per step / term", err.tolist())
-    print("C1 trajectory: fp32 oracle rel gap per step / term", gap32.tolist())
     keys = list(ref_m)
     flat = lambda dd, ks: np.concatenate([np.asarray(dd[k], np.float64).reshape(-1) for k in ks])
     w0 = flat(p0, keys)
-    print("C1 trajectory: w3 - w0 rel err native", _rel(flat(nat_p, keys) - w0, flat(ref_p, keys) - w0),
-          "fp32 oracle", _rel(flat(p32, keys) - w0, flat(ref_p, keys) - w0),
-          "momentum native", _rel(flat(nat_m, keys), flat(ref_m, keys)),
-          "fp32 oracle", _rel(flat(m32, keys), flat(ref_m, keys)))
+    dw = (_rel(flat(nat_p, keys) - w0, flat(ref_p, keys) - w0), _rel(flat(p32, keys) - w0, flat(ref_p, keys) - w0))
+    dm = (_rel(flat(nat_m, keys), flat(ref_m, keys)), _rel(flat(m32, keys), flat(ref_m, keys)))
+    print("C1 trajectory: native rel err per step / term", err.tolist())
+    print("C1 trajectory: fp32 oracle rel gap per step / term", gap32.tolist())
+    print("C1 trajectory: w3 - w0 rel err native / fp32 oracle", dw, "momentum", dm)
     assert [tuple(c) for c in counts] == ref_c, (counts, ref_c)
-    assert np.all(err <= 1e-3), (err.tolist(), gap32.tolist())
+    assert np.all(err[0] <= 1e-3), err[0]
+    assert np.all(err[1:] <= np.maximum(1e-3, 2 * gap32[1:])), (err.tolist(), gap32.tolist())
+    assert gap32[1:].max() > 1e-3, gap32.tolist()
+    assert dw[0] <= 1.5 * dw[1] and dm[0] <= 1.5 * dm[1], (dw, dm)
