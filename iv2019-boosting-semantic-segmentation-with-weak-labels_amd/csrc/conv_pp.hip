@@ -43,8 +43,11 @@ __device__ unsigned long long g_pp_dbg[256 * 16 * 4];
 // K-tile (loop top, before / after barrier A, after the first MFMA segment, after barrier B,
 // before / after barrier C, after the second MFMA segment)
 __device__ unsigned long long g_nt_dbg[8 * 8 * 8 * 8];
+#ifndef NT_DBG_IT
+#define NT_DBG_IT 0   // which tile of the persistent loop is stamped
+#endif
 #define NT_TS(kb, k)                                                                             \
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 8 && dbg_it == 0 && (kb) >= nt_kb0 && (kb) < nt_kb0 + 8) \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 8 && dbg_it == NT_DBG_IT && (kb) >= nt_kb0 && (kb) < nt_kb0 + 8) \
     g_nt_dbg[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + ((kb) - nt_kb0)) * 8 + (k)] =            \
         __builtin_amdgcn_s_memtime()
 #else
