@@ -30,9 +30,11 @@
 
 #ifdef PP_DBG_TIMING
 // A/B only: per-block, per-tile timestamps (s_memtime) of the NT persistent loop
-__device__ unsigned long long g_pp_dbg[256 * 16 * 4];
+// (stamps 0-3: tile start, main loop done, prologue issued, epilogue done; 4-11: per column half
+// qn the staging writes, statistics, staging barrier and stores, at 4 + 4 qn + 0..3)
+__device__ unsigned long long g_pp_dbg[256 * 16 * 16];
 #define PP_TS(it, k) \
-  if (threadIdx.x == 0 && blockIdx.x < 256 && (it) < 16) g_pp_dbg[(blockIdx.x * 16 + (it)) * 4 + (k)] = __builtin_amdgcn_s_memtime()
+  if (threadIdx.x == 0 && blockIdx.x < 256 && (it) < 16) g_pp_dbg[(blockIdx.x * 16 + (it)) * 16 + (k)] = __builtin_amdgcn_s_memtime()
 #else
 #define PP_TS(it, k)
 #endif
@@ -606,9 +608,12 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
             *(u32x2_t*)(stg + row * 256 + ((ch ^ (row & 15)) << 4) + (lq & 1) * 8) = pack4(acc[qm][qn][i][j]);
           }
       }
+      PP_TS(dbg_it, 4 + 4 * qn);
       if (a.stats && nvalid > 0) stats_half(qn);
+      PP_TS(dbg_it, 5 + 4 * qn);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       pp_barrier();
+      PP_TS(dbg_it, 6 + 4 * qn);
       u32x4_t v[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -642,6 +647,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         const long m = m0 + k * 32 + s_row;
         if (m < M && n < a.Co) __builtin_nontemporal_store(v[k], (u32x4_t*)(Y + (size_t)m * a.ldy + n));
       }
+      PP_TS(dbg_it, 7 + 4 * qn);
       if (qn == 0) {   // the second half overwrites the staging area
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         pp_barrier();
