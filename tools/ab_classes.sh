@@ -8,9 +8,6 @@ for r in $(seq ${REPS:-3}); do
   for v in default "$@"; do
     if [ "$v" = default ]; then unset SEG_HIP_LIB; else export SEG_HIP_LIB=$PWD/ab/$v/libseg_hip.so; fi
     timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-eval --no-train-py > gpurun_out/abc.log 2>&1 || exit 1
-    tail -1 gpurun_out/abc.log | python3 -c '
-import json, sys
-d = json.loads(sys.stdin.read()); c = d["roofline"]["classes_ms_per_step"]
-print(sys.argv[1], d["value"], d["ms_per_step"], " ".join(f"{k.split()[0]}={v}" for k, v in c.items()))' "$v" >> "$out"
+    tail -1 gpurun_out/abc.log | python3 tools/ab_line.py "$v" >> "$out"
   done
 done
