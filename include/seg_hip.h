@@ -270,6 +270,14 @@ int seg_op_conv_stat_rows(int dtype, int N, int H, int W, int C, int ldx, int Co
 int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
                       const void* w, int Ci, int k, int stride, int rate, int explicit_pad,
                       int H, int W, void* dx, int lddx, void* stream);
+/* a 1 x 1 stride-1 data gradient with the identity units' epilogue: dx = dgrad(dy) + r (r may
+ * be NULL; it may alias dx), stored masked by omask (ReLU bits [M][Ci/8], bit e of byte n/8 =
+ * channel n; NULL = unmasked) -- the one-tile launches of the pre-masked residual chain
+ * (pre-masked identity-unit gradients, staged residuals); 16-bit dtypes take the
+ * ping-pong kernel for Ci > 128 */
+int seg_op_conv_dgrad_res(int dtype, const void* dy, int N, int H, int W, int Co, int lddy,
+                          const void* wt, int Ci, void* dx, int lddx, const void* r, int ldr,
+                          const uint8_t* omask, void* stream);
 int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
                       const void* x, int H, int W, int Ci, int ldx, int k, int stride, int rate,
                       int explicit_pad, float* dw, void* workspace, int64_t ws_bytes,

@@ -2530,6 +2530,21 @@ int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, 
   return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_dgrad");
 }
 
+int seg_op_conv_dgrad_res(int dtype, const void* dy, int N, int H, int W, int Co, int lddy,
+                          const void* wt, int Ci, void* dx, int lddx, const void* r, int ldr,
+                          const uint8_t* omask, void* stream) {
+  if (!r && !omask) return set_err(nullptr, -EINVAL, "dgrad_res: a residual or a mask is required");
+  if (omask && Ci % 8) return set_err(nullptr, -EINVAL, "dgrad_res: masked outputs need Ci %% 8 == 0");
+  ConvArgs a{};
+  a.x = dy; a.N = N; a.H = H; a.W = W; a.C = Co; a.ldx = lddy;
+  a.w = wt; a.ldw = Co; a.y = dx; a.Ho = H; a.Wo = W; a.Co = Ci; a.ldy = lddx;
+  a.KH = a.KW = 1; a.sf = 1; a.st = 1; a.dil = 1;
+  if (r) { a.r = r; a.ldr = ldr; }
+  if (omask) { a.omask = omask; a.ldm = Ci / 8; }
+  hipError_t e = launch_conv_nt(dt_of(dtype), 0, a, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(nullptr, e, "seg_op_conv_dgrad_res");
+}
+
 int seg_op_conv_wgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, int lddy,
                       const void* x, int H, int W, int Ci, int ldx, int k, int stride, int rate,
                       int explicit_pad, float* dw, void* workspace, int64_t ws_bytes, void* stream) {

@@ -24,6 +24,7 @@ EXPORTED_SYMBOLS = [
     "seg_backward", "seg_apply_update", "seg_outputs", "seg_confusion", "seg_debug_tensor",
     "seg_profile", "seg_profile_dump",
     "seg_profile_read", "seg_op_conv_fwd", "seg_op_conv_stat_rows", "seg_op_conv_dgrad",
+    "seg_op_conv_dgrad_res",
     "seg_op_conv_wgrad", "seg_op_conv_wgrad_cfg", "seg_bbox_labels", "seg_tag_labels",
     "seg_grad_buckets", "seg_stream_wait_bucket", "seg_set_loss_scale", "seg_found_inf",
     "seg_set_bn_sync", "seg_set_bn_inference", "seg_predict", "seg_full_predictions",
@@ -100,6 +101,7 @@ def _load():
         "seg_op_conv_stat_rows": (ip, [ip] * 12),
         "seg_op_conv_dgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, vp,
                                    ip, vp]),
+        "seg_op_conv_dgrad_res": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, vp, ip, vp, ip, vp, vp]),
         "seg_op_conv_wgrad": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip, ip,
                                    vp, vp, i64, vp]),
         "seg_op_conv_wgrad_cfg": (ip, [ip, vp, ip, ip, ip, ip, ip, vp, ip, ip, ip, ip, ip, ip, ip,

@@ -152,6 +152,65 @@ def test_conv_dgrad(cuda, dtype, case):
     assert _rel(dx.float().cpu().numpy(), ref) < TOL[dtype]
 
 
+# the identity units' data-gradient epilogue (seg_op_conv_dgrad_res): N, H, W, Co (= the
+# forward conv's output channels: dy's), Ci (dx's), with residual, with the consumer's ReLU bits
+RES_CASES = [
+    (2, 16, 32, 256, 512, True, True),     # one-tile ping-pong launch: residual + mask (4 x 2 tiles)
+    (2, 16, 32, 256, 512, True, False),    # residual only
+    (1, 20, 20, 128, 256, True, True),     # ragged rows (400 pixels), K 128
+    (1, 16, 16, 64, 256, False, True),     # mask only (the premasked dgrad without residual), K 64
+    (2, 8, 16, 512, 2048, True, True),     # the block4 shape class: K 512 -> N 2048
+    (1, 12, 20, 256, 128, True, False),    # Ci <= 128: the v2 kernel's residual epilogue
+]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", RES_CASES)
+def test_conv_dgrad_residual_masked(cuda, dtype, case):
+    """dx = round(round(dgrad(dy)) + r), stored with the outputs whose ReLU bit is 0 set to
+    zero (pre-masked identity-unit gradients, staged residuals -- the identity units'
+    conv1 data gradient), against a float64 restatement on the same 16-bit operands: kept
+    elements at the 16-bit bound of the other op tests (L2-relative), masked-off elements exactly
+    zero, the residual read in place (r aliasing dx) bitwise the same as from another buffer."""
+    from seg_hip import LIB, check
+    N, H, W, Co, Ci, with_r, with_m = case
+    g = np.random.default_rng(7)
+    dy = _round(g.standard_normal((N, H, W, Co)).astype(np.float32), dtype)
+    w = _round((g.standard_normal((Co, Ci)) * np.sqrt(2.0 / Ci)).astype(np.float32), dtype)
+    res = _round(g.standard_normal((N, H, W, Ci)).astype(np.float32), dtype) if with_r else None
+    bits = g.integers(0, 256, size=(N, H, W, Ci // 8), dtype=np.uint8) if with_m else None
+    dg = np.einsum("nhwo,oi->nhwi", dy.astype(np.float64), w.astype(np.float64))
+    tdt = TDT[dtype]
+    ref = dg
+    if with_r:   # the kernel rounds the data gradient to 16 bits, then adds the residual
+        ref = torch.as_tensor(dg).to(tdt).double().numpy() + res
+    keep = np.ones((N, H, W, Ci), bool)
+    if with_m:
+        keep = ((bits[..., :, None] >> np.arange(8)) & 1).astype(bool).reshape(N, H, W, Ci)
+    st = torch.cuda.current_stream().cuda_stream
+    dyd = torch.as_tensor(dy).to(cuda, tdt).contiguous()
+    wtd = torch.as_tensor(np.ascontiguousarray(w.T)).to(cuda, tdt).contiguous()   # [Ci][Co]
+    md = torch.as_tensor(bits).to(cuda).contiguous() if with_m else None
+    outs = []
+    for alias in ((False, True) if with_r else (False,)):
+        if alias:
+            dx = torch.as_tensor(res).to(cuda, tdt).contiguous()
+            rd = dx
+        else:
+            dx = torch.full((N, H, W, Ci), 7.0, dtype=tdt, device=cuda)
+            rd = torch.as_tensor(res).to(cuda, tdt).contiguous() if with_r else None
+        check(LIB.seg_op_conv_dgrad_res(ABI[dtype], dyd.data_ptr(), N, H, W, Co, Co, wtd.data_ptr(), Ci,
+                                        dx.data_ptr(), Ci, rd.data_ptr() if rd is not None else None, Ci,
+                                        md.data_ptr() if md is not None else None, st))
+        torch.cuda.synchronize()
+        outs.append(dx.float().cpu().numpy())
+    for got in outs:
+        assert np.all(got[~keep] == 0.0)
+        assert _rel(got[keep], ref[keep]) < TOL[dtype]
+    if len(outs) == 2:
+        assert np.array_equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("case", CASES)
 def test_conv_wgrad(cuda, dtype, case):

@@ -1,5 +1,5 @@
 """Single-op timing of the conv kernels at C2 layer shapes (GPU box):
-    python tools/op_bench.py [fwd|dgrad|wgrad] [layer]   (layer: b4c2, b4c3, b3c2, b4c1)
+    python tools/op_bench.py [fwd|dgrad|dgradres|wgrad] [layer]   (layer: b4c2, b4c3, b3c2, b4c1)
 Used under rocprofv3 --pmc for counter passes on one kernel class."""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -35,11 +35,18 @@ st = torch.empty((N * H * W + 63) // 64 * Co * 2, device=dev, dtype=torch.float3
 dw = torch.empty(Co * k * k * Ci, device=dev, dtype=torch.float32)
 ws = torch.empty(512 << 20, device=dev, dtype=torch.uint8)
 wt = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+if op == "dgradres":
+    assert k == 1 and s == 1
+    res = torch.randn(N, H, W, Ci, generator=g).to(dev, torch.bfloat16)
+    bits = torch.randint(0, 256, (N, H, W, Ci // 8), generator=g, dtype=torch.uint8).to(dev)
 stream = torch.cuda.current_stream().cuda_stream
 def run():
     if op == "fwd":
         check(LIB.seg_op_conv_fwd(1, x.data_ptr(), N, H, W, Ci, Ci, w.data_ptr(), Co, k, s, r, 0,
                                   y.data_ptr(), Co, 0 if os.environ.get("NOSTATS") else st.data_ptr(), stream))
+    elif op == "dgradres":   # the identity units' conv1 data gradient: + residual, premasked
+        check(LIB.seg_op_conv_dgrad_res(1, dy.data_ptr(), N, H, W, Co, Co, wt.data_ptr(), Ci,
+                                        dx.data_ptr(), Ci, res.data_ptr(), Ci, bits.data_ptr(), stream))
     elif op == "dgrad":
         check(LIB.seg_op_conv_dgrad(1, dy.data_ptr(), N, H, W, Co, Co, wt.data_ptr(), Ci, k, s, r, 0,
                                     H, W, dx.data_ptr(), Ci, stream))
