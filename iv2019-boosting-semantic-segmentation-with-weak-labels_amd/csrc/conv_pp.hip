@@ -124,7 +124,8 @@ __device__ __forceinline__ void row_total8(float (&v)[8]) {
 
 // PERSIST: 1 = loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
 // epilogue; 0 = one tile per workgroup (the residual-epilogue launches: their register
-// budget goes to the residual prefetch instead of the next tile's address state)
+// budget goes to the residual prefetch instead of the next tile's address state); 2 = one
+// tile, dense 1 x 1 rows with one residual fetched by LDS-DMA (RQ below)
 template <typename E, int ST, int PERSIST>
 __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   typedef typename Half<E>::V V;
@@ -332,20 +333,60 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     issue_half(0, t0, 3);
     issue_half(0, t0, 1);
   };
+  // RQ (round 6): the one-tile residual data gradients (dense 1 x 1 rows, one residual: the
+  // identity units' conv1, DESIGN.md staged residuals) take their residual by LDS-DMA instead
+  // of global loads in the epilogue, whose latency the per-tile stamps showed exposed (epilogue
+  // 21k cycles against 6k without a residual, profiles/r06_residual_epilogue.txt): quarters 0-1
+  // of the residual tile (64 columns = 32 KB each) stream into the K-tile buffer the last K-tile
+  // does not read, during that K-tile; quarters 2-3 into the other buffer as soon as the main
+  // loop ends; the epilogue runs per 64-column quarter through the 32 KB above the two K-tile
+  // buffers (staging) and reads the staged outputs and the residual at the same row / chunk.
+  // The sum is unchanged: round(round(dgrad) + r), then the consumer's ReLU bits
+  constexpr bool RQ_OK = PERSIST == 2;
+  static_assert(!RQ_OK || ST == 0, "RQ: dense 1 x 1 rows only");
+  constexpr bool rq = RQ_OK;   // pp_launch_st: a.r set, a.r2 not, M * ldr * 2 < 2^31
+  const auto rs_r = __builtin_amdgcn_make_buffer_rsrc((void*)a.r, (short)0,
+                                                      (int)(rq ? (long)M * a.ldr * 2 : 0), 0x00020000);
+  // 32 pieces of 8 rows x 128 B per quarter, 4 per wave; LDS [row][8 chunks] unswizzled
+  auto issue_res = [&](int Q, char* dst) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = wave * 4 + i;
+      const int row = p * 8 + (lane >> 3);
+      const int ch = n0 + Q * 64 + (lane & 7) * 8;
+      const long m = m0 + row;
+      const uint32_t off = m < M && ch < a.Co ? (uint32_t)((m * a.ldr + ch) * 2) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_r, (__attribute__((address_space(3))) void*)(dst + p * 1024),
+                                               16, off, 0, 0, 0);
+    }
+  };
   // consumer ReLU bits (ConvArgs::omask, one-tile launches): one byte per 16-B chunk the
-  // epilogue stores (rows k * 32 + tid / 16, chunk tid % 16 of each 128-column half), loaded
+  // epilogue stores, one to a register (packing them would wait for the loads here), loaded
   // before the first K-tile so their latency hides behind the main loop (loaded in the
-  // epilogue, their latency cost ~4 us per tile: block4 conv1 dgrad +20 %)
-  uint32_t mb[2][8];
-  const bool omask = PERSIST == 0 && a.omask;   // wave-uniform
-  if (omask) {
+  // epilogue, their latency cost ~4 us per tile: block4 conv1 dgrad +20 %). RQ: quarter Q,
+  // pass k (row k * 64 + tid / 8, chunk tid % 8 of the quarter) in mb[Q * 4 + k], all ones
+  // without a mask; otherwise half qn, pass k (rows k * 32 + tid / 16, chunk tid % 16 of the
+  // half) in mb[qn * 8 + k]
+  uint32_t mb[16];
+  const bool omask = PERSIST != 1 && a.omask;   // wave-uniform
+  if constexpr (RQ_OK) {
+#pragma unroll
+    for (int Q = 0; Q < 4; ++Q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const long m = m0 + k * 64 + (tid >> 3);
+        const int n = n0 + Q * 64 + (tid & 7) * 8;
+        mb[Q * 4 + k] = !omask ? ~0u : m < M && n < a.Co ? a.omask[(size_t)m * a.ldm + (n >> 3)] : 0u;
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  } else if (omask) {
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const long m = m0 + k * 32 + (tid >> 4);
         const int n = n0 + qn * 128 + (tid & 15) * 8;
-        mb[qn][k] = m < M && n < a.Co ? a.omask[(size_t)m * a.ldm + (n >> 3)] : 0u;
+        mb[qn * 8 + k] = m < M && n < a.Co ? a.omask[(size_t)m * a.ldm + (n >> 3)] : 0u;
       }
     __builtin_amdgcn_sched_barrier(0);   // keep the loads here, ahead of the prologue's DMA
   }
@@ -398,9 +439,15 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         issue_half(kb + 1, tn1, 2);
         issue_half(kb + 1, tn1, 1);
       }
+      if constexpr (RQ_OK) {
+        if (rq && !m1) {   // the last K-tile: residual quarters 0-1 into the buffer it does not read
+          issue_res(0, smem + (nk & 1) * BUF);
+          issue_res(1, smem + (nk & 1) * BUF + 32768);
+        }
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (wm == 1) {
-        if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (m1 || rq) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // (rq: its 8 residual pieces)
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       NT_TS(kb, 1);
@@ -409,7 +456,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       mfma_q(0, 0);
       mfma_q(0, 1);
       if (wm == 0) {
-        if (m1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (m1 || rq) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       NT_TS(kb, 3);
@@ -580,9 +627,79 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     // (round 3: they were read in the accumulator layout, 8 B per lane from 16 rows per load,
     // a quadrant at a time, and added before the single rounding: the short-K residual data
     // gradients 6-8 % slower, the step -0.6 %; profiles/r03_res_staged.txt)
+    if constexpr (RQ_OK) {
+      if (rq) {
+        char* const bfree = smem + (nk & 1) * BUF;         // quarters 0-1 (the last K-tile's DMA)
+        char* const blast = smem + ((nk - 1) & 1) * BUF;   // quarters 2-3, free from here on
+        issue_res(2, blast);
+        issue_res(3, blast + 32768);
+        char* const sq = smem + PP_LDS;                    // one quarter's staged outputs
+        const int q_row = tid >> 3, q_ch = tid & 7;
+        // every store of the tile issues (4 per thread and quarter): the vmcnt below may count
+        // them; otherwise only the younger quarters' DMA pieces are counted (conservative)
+        const bool fullt = m0 + BM <= M && n0 + BN <= a.Co;
+#pragma unroll
+        for (int Q = 0; Q < 4; ++Q) {
+          const int qn = Q >> 1;
+          if ((wn >> 1) == (Q & 1)) {   // the 4 waves that hold columns Q * 64 .. + 63
+#pragma unroll
+            for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                  const int row = wm * 128 + qm * 64 + i * 16 + lr;
+                  const int ch = (wn & 1) * 4 + j * 2 + (lq >> 1);
+                  *(u32x2_t*)(sq + row * 128 + ((ch ^ (row & 7)) << 4) + (lq & 1) * 8) = pack4(acc[qm][qn][i][j]);
+                }
+          }
+          // this wave's pieces of residual quarter Q landed (the barrier covers the others')
+          if (fullt) {
+            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+          } else {
+            if (Q == 0) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            if (Q == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            if (Q == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            if (Q == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          pp_barrier();
+          PP_TS(dbg_it, 4 + 2 * Q);
+          const char* const rsrc = (Q < 2 ? bfree : blast) + (Q & 1) * 32768;
+          u32x4_t v[4], rr[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int row = k * 64 + q_row;
+            v[k] = *(const u32x4_t*)(sq + row * 128 + ((q_ch ^ (row & 7)) << 4));
+            rr[k] = *(const u32x4_t*)(rsrc + row * 128 + q_ch * 16);
+          }
+          const int n = n0 + Q * 64 + q_ch * 8;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t bk = mb[Q * 4 + k];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              const uint32_t x = v[k][w], r = rr[k][w];
+              const float lo = TypeOps<E>::to_f(lo16<E>(x)) + TypeOps<E>::to_f(lo16<E>(r));
+              const float hi = TypeOps<E>::to_f(hi16<E>(x)) + TypeOps<E>::to_f(hi16<E>(r));
+              const uint32_t b = bk >> (2 * w);
+              v[k][w] = pack2<E>(lo, hi) & (((b & 1u) ? 0x0000ffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u));
+            }
+            const long m = m0 + k * 64 + q_row;
+            if (m < M && n < a.Co) __builtin_nontemporal_store(v[k], (u32x4_t*)(Y + (size_t)m * a.ldy + n));
+          }
+          PP_TS(dbg_it, 5 + 2 * Q);
+          if (Q < 3) {   // the next quarter overwrites the staging area
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            pp_barrier();
+          }
+        }
+        goto rq_done;
+      }
+    }
     const E* R1 = (const E*)a.r;
     const E* R2 = (const E*)a.r2;
-    const int nres = PERSIST ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
+    const int nres = PERSIST == 1 ? 0 : (R1 ? 1 : 0) + (R2 ? 1 : 0);   // wave-uniform
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn) {
       u32x4_t rs1[8], rs2[8];
@@ -638,7 +755,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         for (int k = 0; k < 8; ++k)
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
-            const uint32_t b = mb[qn][k] >> (2 * w);
+            const uint32_t b = mb[qn * 8 + k] >> (2 * w);
             v[k][w] &= ((b & 1u) ? 0x0000ffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
           }
       }
@@ -654,6 +771,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       }
     }
   }
+rq_done:
   PP_TS(dbg_it, 3);
   ++dbg_it;
   if (!has_next) break;
@@ -684,8 +802,9 @@ int pp_grid(int nwg) {
 
 template <typename E, int ST, int PERSIST>
 hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
-  // two K-tile buffers (the epilogue stages through buffer 1)
-  constexpr int LDS = PP_LDS;
+  // two K-tile buffers (the epilogue stages through buffer 1); the one-tile dense 1x1 launches
+  // also the 32 KB quarter staging of the residual epilogue (RQ)
+  constexpr int LDS = PP_LDS + (PERSIST == 2 ? 32768 : 0);
   auto kern = conv_nt_pp_kernel<E, ST, PERSIST>;
   static bool attr = false;
   if (!attr) {
@@ -699,8 +818,15 @@ hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifndef PP_RQ
+#define PP_RQ 1   // 0: the RQ launches take the one-tile epilogue's global residual loads (A/B)
+#endif
+
 template <typename E, int ST>
 hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
+  if constexpr (ST == 0 && PP_RQ) {
+    if (a.r && !a.r2 && (long)a.N * a.Ho * a.Wo * a.ldr * 2 < (1L << 31)) return pp_launch<E, 0, 2>(a, s);
+  }
   if (a.r || a.r2 || a.omask) return pp_launch<E, ST, 0>(a, s);
   return pp_launch<E, ST, 1>(a, s);
 }

@@ -18,13 +18,24 @@ ph = {"main": [], "stats": [], "epi": [], "gap": []}
 # the epilogue's pieces (stamps 4-11): per column half the staging writes (from the previous
 # stamp), statistics, staging barrier, staging reads + stores
 sub = {f"q{q}_{n}": [] for q in (0, 1) for n in ("stage", "stats", "bar", "store")}
+# RQ=1 (the one-tile residual epilogue, four 64-column quarters): stamps 4 + 2Q after the
+# quarter's staging writes, residual wait and barrier, 5 + 2Q after its stores
+RQ = os.environ.get("RQ") == "1"
+if RQ:
+    sub = {f"Q{q}_{n}": [] for q in range(4) for n in ("stage_wait", "store")}
 for b in range(256):
     for i in range(n[b]):
         r = t[b, i]
         ph["main"].append(r[1] - r[0]); ph["stats"].append(r[2] - r[1]); ph["epi"].append(r[3] - r[2])
         if i + 1 < n[b]:
             ph["gap"].append(t[b, i + 1, 0] - r[3])
-        if r[4] > 0:
+        if r[4] > 0 and RQ:
+            prev = r[2]
+            for q in range(4):
+                for j, nm in enumerate(("stage_wait", "store")):
+                    sub[f"Q{q}_{nm}"].append(r[4 + 2 * q + j] - prev)
+                    prev = r[4 + 2 * q + j]
+        elif r[4] > 0:
             prev = r[2]
             for q in (0, 1):
                 for j, nm in enumerate(("stage", "stats", "bar", "store")):
