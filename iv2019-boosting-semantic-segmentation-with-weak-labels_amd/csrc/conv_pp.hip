@@ -124,8 +124,8 @@ __device__ __forceinline__ void row_total8(float (&v)[8]) {
 
 // PERSIST: 1 = loop over tiles (grid = CU count) with the next tile's first DMA overlapping the
 // epilogue; 0 = one tile per workgroup (the residual-epilogue launches: their register
-// budget goes to the residual prefetch instead of the next tile's address state); 2 = one
-// tile, dense 1 x 1 rows with one residual fetched by LDS-DMA (RQ below)
+// budget goes to the residual prefetch instead of the next tile's address state); 3 =
+// persistent, dense 1 x 1 rows with one residual fetched by LDS-DMA (RQP below)
 template <typename E, int ST, int PERSIST>
 __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   typedef typename Half<E>::V V;
@@ -161,6 +161,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   constexpr bool dual = ST == 4;
   const int nk = (a.KH * a.KW * a.C) / PBK + (dual ? a.C2 / PBK : 0);
   const int ntaps = a.KH * a.KW;
+  // K-tile kb of the current tile is in buffer (kb + par) % 2; RQP starts a tile in whichever
+  // buffer its predecessor's epilogue freed first (always 0 otherwise)
+  int par = 0;
   const E* X = (const E*)a.x;
   const E* Wt = (const E*)a.w;
 
@@ -257,7 +260,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
 
   // half ids: 0 = A0, 1 = A1, 2 = B0, 3 = B1 (LDS offset hid * HALF inside a K-tile buffer)
   auto issue_half = [&](int kb, const KT& t, int hid, int i0 = 0, int i1 = 2) {
-    char* dst = smem + (kb & 1) * BUF + hid * HALF;
+    char* dst = smem + ((kb + par) & 1) * BUF + hid * HALF;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i < i0 || i >= i1) continue;
@@ -333,51 +336,64 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     issue_half(0, t0, 3);
     issue_half(0, t0, 1);
   };
-  // RQ (round 6): the one-tile residual data gradients (dense 1 x 1 rows, one residual: the
-  // identity units' conv1, DESIGN.md staged residuals) take their residual by LDS-DMA instead
-  // of global loads in the epilogue, whose latency the per-tile stamps showed exposed (epilogue
-  // 21k cycles against 6k without a residual, profiles/r06_residual_epilogue.txt): quarters 0-1
-  // of the residual tile (64 columns = 32 KB each) stream into the K-tile buffer the last K-tile
-  // does not read, during that K-tile; quarters 2-3 into the other buffer as soon as the main
-  // loop ends; the epilogue runs per 64-column quarter through the 32 KB above the two K-tile
-  // buffers (staging) and reads the staged outputs and the residual at the same row / chunk.
-  // The sum is unchanged: round(round(dgrad) + r), then the consumer's ReLU bits
-  constexpr bool RQ_OK = PERSIST == 2;
-  static_assert(!RQ_OK || ST == 0, "RQ: dense 1 x 1 rows only");
-  constexpr bool rq = RQ_OK;   // pp_launch_st: a.r set, a.r2 not, M * ldr * 2 < 2^31
+  // RQP (round 6): the residual data gradients (dense 1 x 1 rows, one residual: the identity
+  // units' conv1, DESIGN.md staged residuals) run persistent, the residual tile fetched by
+  // LDS-DMA instead of global loads in the epilogue, whose latency the per-tile stamps showed
+  // exposed (one-tile launches: epilogue 21k cycles against 6k without a residual,
+  // profiles/r06_s18_rqp.txt): the tile's column half 0 (128 columns, 64 KB) streams into the
+  // K-tile buffer the last K-tile does not read, during that K-tile; half 1 into the other
+  // buffer as soon as the main loop ends. Each wave adds its accumulators to the residual in
+  // place, in the accumulator layout, then every wave streams rows out of the sums; once half
+  // 0's rows are out, the next tile's mask bytes and K-tile 0 go into its buffer, in flight
+  // during half 1. dx = round(dgrad + r) (one rounding), then the consumer's ReLU bits
+  constexpr bool RQP = PERSIST == 3;
+  static_assert(!RQP || ST == 0, "RQP: dense 1 x 1 rows only");
+  // pp_launch_st: a.r set, a.r2 not, M * ldr * 2 < 2^31
   const auto rs_r = __builtin_amdgcn_make_buffer_rsrc((void*)a.r, (short)0,
-                                                      (int)(rq ? (long)M * a.ldr * 2 : 0), 0x00020000);
-  // 32 pieces of 8 rows x 128 B per quarter, 4 per wave; LDS [row][8 chunks] unswizzled
-  auto issue_res = [&](int Q, char* dst) {
+                                                      (int)(RQP ? (long)M * a.ldr * 2 : 0), 0x00020000);
+  // Each wave fetches exactly the residual it adds in place -- rows wm * 128 .. + 127, columns wn * 32 .. + 31 of a 128-column half: 8
+  // pieces of 16 rows x 64 B. LDS: half = 4 column groups (wn) of 256 rows x 64 B; 16-B chunk
+  // s of row r at slot s ^ ((r / 4) % 4): conflict-free 8-B accesses for the 16 rows of a
+  // fragment and 16-B reads of 4 rows x 4 groups per instruction
+  // offsets: a lane part (tile-independent, one register) plus a wave-uniform part; rows past
+  // M fall past the buffer's end (zeros), columns past Co are read but never stored
+  const uint32_t rw_lane = RQP ? (uint32_t)(((lane >> 2) * a.ldr + (((lane & 3) ^ ((lane >> 4) & 3)) << 3)) * 2) : 0u;
+  auto issue_resw = [&](int hh, char* dst) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = wave * 4 + i;
-      const int row = p * 8 + (lane >> 3);
-      const int ch = n0 + Q * 64 + (lane & 7) * 8;
-      const long m = m0 + row;
-      const uint32_t off = m < M && ch < a.Co ? (uint32_t)((m * a.ldr + ch) * 2) : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_r, (__attribute__((address_space(3))) void*)(dst + p * 1024),
-                                               16, off, 0, 0, 0);
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t sb = (uint32_t)((((int)m0 + wm * 128 + i * 16) * a.ldr + n0 + hh * 128 + wn * 32) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs_r, (__attribute__((address_space(3))) void*)(dst + wn * 16384 + (wm * 128 + i * 16) * 64), 16, rw_lane + sb, 0, 0, 0);
     }
   };
-  // consumer ReLU bits (ConvArgs::omask, one-tile launches): one byte per 16-B chunk the
-  // epilogue stores, one to a register (packing them would wait for the loads here), loaded
-  // before the first K-tile so their latency hides behind the main loop (loaded in the
-  // epilogue, their latency cost ~4 us per tile: block4 conv1 dgrad +20 %). RQ: quarter Q,
-  // pass k (row k * 64 + tid / 8, chunk tid % 8 of the quarter) in mb[Q * 4 + k], all ones
-  // without a mask; otherwise half qn, pass k (rows k * 32 + tid / 16, chunk tid % 16 of the
-  // half) in mb[qn * 8 + k]
+  // RQP: the consumer's ReLU bytes of the chunks a thread stores (row k * 32 + wave * 4 +
+  // (lane / 4) % 4, chunk 4 * (lane / 16) + lane % 4 of half qn), by byte buffer loads (rows
+  // past M read 0)
+  const auto rs_m = __builtin_amdgcn_make_buffer_rsrc((void*)a.omask, (short)0,
+                                                      (int)(RQP && a.omask ? M * a.ldm : 0), 0x00020000);
+  const uint32_t mk_lane = RQP ? (uint32_t)(((lane >> 2) & 3) * a.ldm + (lane >> 4) * 4 + (lane & 3)) : 0u;
+  auto load_mask = [&](long m0_, int n0_, uint32_t (&mbx)[16]) {
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t sb = (uint32_t)(((int)m0_ + k * 32 + wave * 4) * a.ldm + ((n0_ + qn * 128) >> 3));
+        mbx[qn * 8 + k] = __builtin_amdgcn_raw_buffer_load_b8(rs_m, mk_lane + sb, 0, 0);
+      }
+  };
+  // consumer ReLU bits (ConvArgs::omask, one-tile and RQP launches): one byte per 16-B chunk
+  // the epilogue stores, one to a register (packing them would wait for the loads here), loaded
+  // before the K-tile 0 DMA so their latency hides behind it and the main loop (loaded in the
+  // epilogue, their latency cost ~4 us per tile: block4 conv1 dgrad +20 %): half qn, pass k
+  // in mb[qn * 8 + k] (one-tile: rows k * 32 + tid / 16, chunk tid % 16 of the half; RQP:
+  // load_mask), all ones in RQP launches without a mask
   uint32_t mb[16];
   const bool omask = PERSIST != 1 && a.omask;   // wave-uniform
-  if constexpr (RQ_OK) {
+  if constexpr (RQP) {
+    if (omask) load_mask(m0, n0, mb);
+    else
 #pragma unroll
-    for (int Q = 0; Q < 4; ++Q)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const long m = m0 + k * 64 + (tid >> 3);
-        const int n = n0 + Q * 64 + (tid & 7) * 8;
-        mb[Q * 4 + k] = !omask ? ~0u : m < M && n < a.Co ? a.omask[(size_t)m * a.ldm + (n >> 3)] : 0u;
-      }
+      for (int k = 0; k < 16; ++k) mb[k] = ~0u;
     __builtin_amdgcn_sched_barrier(0);
   } else if (omask) {
 #pragma unroll
@@ -405,6 +421,14 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   // A0, B0 of K-tile 0 landed (B1, A1 in flight; a previous tile's epilogue stores, issued
   // after them, count too and are waited for here)
   asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // A0, B0, B1 landed (A1 in flight)
+  // RQP: the tile's mask bytes (issued before its K-tile 0) landed too: four to a register
+  // through the main loop
+  uint32_t mp[4];
+  if constexpr (RQP) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      mp[q] = (mb[4 * q] & 0xffu) | (mb[4 * q + 1] & 0xffu) << 8 | (mb[4 * q + 2] & 0xffu) << 16 | mb[4 * q + 3] << 24;
+  }
   pp_barrier();
   if (wm == 1) pp_barrier();   // stagger: wave row 1 runs one segment behind
   // the lagging row loses every issue arbitration at equal priority: one static raise for the
@@ -424,7 +448,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     const int nt_kb0 = nk >= 24 ? 16 : 0;
 #endif
     for (int kb = 0; kb < nk; ++kb) {
-      const char* buf = smem + (kb & 1) * BUF;
+      const char* buf = smem + ((kb + par) & 1) * BUF;
       const bool m1 = kb + 1 < nk, m2 = kb + 2 < nk;
       NT_TS(kb, 0);
       read_a(buf, 0);
@@ -439,15 +463,12 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
         issue_half(kb + 1, tn1, 2);
         issue_half(kb + 1, tn1, 1);
       }
-      if constexpr (RQ_OK) {
-        if (rq && !m1) {   // the last K-tile: residual quarters 0-1 into the buffer it does not read
-          issue_res(0, smem + (nk & 1) * BUF);
-          issue_res(1, smem + (nk & 1) * BUF + 32768);
-        }
+      if constexpr (RQP) {   // the last K-tile: residual half 0 into the buffer it does not read
+        if (!m1) issue_resw(0, smem + ((nk + par) & 1) * BUF);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (wm == 1) {
-        if (m1 || rq) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // (rq: its 8 residual pieces)
+        if (m1 || RQP) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // (RQP: its 8 residual pieces)
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       NT_TS(kb, 1);
@@ -456,7 +477,7 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
       mfma_q(0, 0);
       mfma_q(0, 1);
       if (wm == 0) {
-        if (m1 || rq) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (m1 || RQP) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       NT_TS(kb, 3);
@@ -491,9 +512,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   PP_TS(dbg_it, 1);
   // next tile: its K-tile 0 goes into buffer 0 now, in flight during this tile's epilogue
   const int tile_n = tile + (int)gridDim.x;
-  const bool has_next = PERSIST == 1 && tile_n < nwg;
+  const bool has_next = (PERSIST == 1 || RQP) && tile_n < nwg;
   int mt_n = 0, nt_n = 0;
-  if (has_next) {
+  if (PERSIST == 1 && has_next) {
     tile_of(tile_n, mt_n, nt_n);
     setup_lanes((long)mt_n * BM, nt_n * BN);
     prologue();
@@ -627,75 +648,94 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
     // (round 3: they were read in the accumulator layout, 8 B per lane from 16 rows per load,
     // a quadrant at a time, and added before the single rounding: the short-K residual data
     // gradients 6-8 % slower, the step -0.6 %; profiles/r03_res_staged.txt)
-    if constexpr (RQ_OK) {
-      if (rq) {
-        char* const bfree = smem + (nk & 1) * BUF;         // quarters 0-1 (the last K-tile's DMA)
-        char* const blast = smem + ((nk - 1) & 1) * BUF;   // quarters 2-3, free from here on
-        issue_res(2, blast);
-        issue_res(3, blast + 32768);
-        char* const sq = smem + PP_LDS;                    // one quarter's staged outputs
-        const int q_row = tid >> 3, q_ch = tid & 7;
-        // every store of the tile issues (4 per thread and quarter): the vmcnt below may count
-        // them; otherwise only the younger quarters' DMA pieces are counted (conservative)
-        const bool fullt = m0 + BM <= M && n0 + BN <= a.Co;
+    if constexpr (RQP) {
+      char* const hres[2] = {smem + ((nk + par) & 1) * BUF,       // half 0: the last K-tile's DMA
+                             smem + ((nk - 1 + par) & 1) * BUF};  // half 1: free from here on
+      issue_resw(1, hres[1]);
+      // every store of half 0 issues (8 per thread): the wait for half 1 may count them
+      const bool fullt = m0 + BM <= M && n0 + BN <= a.Co;
+      typedef float f32x2_t __attribute__((ext_vector_type(2)));
+      // lane-derived addresses from an opaque zero: hoisted out of the tile loop they were live
+      // through the main loop (spilled)
+      int ez;
+      asm volatile("s_mov_b32 %0, 0" : "=s"(ez));
+      const int lre = lr + ez, lanee = lane + ez;
 #pragma unroll
-        for (int Q = 0; Q < 4; ++Q) {
-          const int qn = Q >> 1;
-          if ((wn >> 1) == (Q & 1)) {   // the 4 waves that hold columns Q * 64 .. + 63
+      for (int qn = 0; qn < 2; ++qn) {
+        char* const hw = hres[qn] + wn * 16384;
+        // this wave's residual of half qn landed (each wave adds only what it fetched); half 1:
+        // half 0's 8 stores, the next tile's 16 mask loads and 8 K-tile-0 pieces are younger
+        if (qn == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (!fullt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (has_next) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        PP_TS(dbg_it, 4 + 3 * qn);
+        // in place, accumulator layout: dx = round(dgrad + r), one rounding
+        u32x2_t rr[2][4][2];
 #pragma unroll
-            for (int qm = 0; qm < 2; ++qm)
+        for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
-              for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                  const int row = wm * 128 + qm * 64 + i * 16 + lr;
-                  const int ch = (wn & 1) * 4 + j * 2 + (lq >> 1);
-                  *(u32x2_t*)(sq + row * 128 + ((ch ^ (row & 7)) << 4) + (lq & 1) * 8) = pack4(acc[qm][qn][i][j]);
-                }
-          }
-          // this wave's pieces of residual quarter Q landed (the barrier covers the others')
-          if (fullt) {
-            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-          } else {
-            if (Q == 0) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-            if (Q == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            if (Q == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            if (Q == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
+            for (int j = 0; j < 2; ++j) {
+              const int row = wm * 128 + qm * 64 + i * 16 + lre;
+              const int sl = j * 2 + (lq >> 1);
+              rr[qm][i][j] = *(const u32x2_t*)(hw + row * 64 + ((sl ^ ((row >> 2) & 3)) << 4) + (lq & 1) * 8);
+            }
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int row = wm * 128 + qm * 64 + i * 16 + lre;
+              const int sl = j * 2 + (lq >> 1);
+              const f32x4_t& x = acc[qm][qn][i][j];
+              u32x2_t o;
+#pragma unroll
+              for (int w = 0; w < 2; ++w) {
+                const uint32_t r = rr[qm][i][j][w];
+                const f32x2_t xs = {x[2 * w], x[2 * w + 1]};
+                const f32x2_t rs = {TypeOps<E>::to_f(lo16<E>(r)), TypeOps<E>::to_f(hi16<E>(r))};
+                const f32x2_t sum = xs + rs;
+                o[w] = pack2<E>(sum[0], sum[1]);
+              }
+              *(u32x2_t*)(hw + row * 64 + ((sl ^ ((row >> 2) & 3)) << 4) + (lq & 1) * 8) = o;
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_barrier();
+        PP_TS(dbg_it, 5 + 3 * qn);
+        // rows out: per instruction 4 rows x 256 B (lane: group lane / 16, row (lane / 4) % 4,
+        // chunk lane % 4 of the group), masked by the consumer's ReLU bits
+        const int g = lanee >> 4, sl = lanee & 3;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int row = k * 32 + wave * 4 + ((lanee >> 2) & 3);
+          u32x4_t v = *(const u32x4_t*)(hres[qn] + g * 16384 + row * 64 + ((sl ^ ((row >> 2) & 3)) << 4));
+          const uint32_t b = mp[qn * 2 + (k >> 2)] >> (8 * (k & 3));
+#pragma unroll
+          for (int w = 0; w < 4; ++w)
+            v[w] &= ((b >> (2 * w)) & 1u ? 0x0000ffffu : 0u) | ((b >> (2 * w)) & 2u ? 0xffff0000u : 0u);
+          const long m = m0 + row;
+          const int n = n0 + qn * 128 + g * 32 + sl * 8;
+          if (m < M && n < a.Co) __builtin_nontemporal_store(v, (u32x4_t*)(Y + (size_t)m * a.ldy + n));
+        }
+        PP_TS(dbg_it, 6 + 3 * qn);
+        if (qn == 0 && has_next) {
+          // half 0's buffer is free once every wave's reads of it are done: the next tile's
+          // mask bytes and K-tile 0 go there, in flight during half 1
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           pp_barrier();
-          PP_TS(dbg_it, 4 + 2 * Q);
-          const char* const rsrc = (Q < 2 ? bfree : blast) + (Q & 1) * 32768;
-          u32x4_t v[4], rr[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int row = k * 64 + q_row;
-            v[k] = *(const u32x4_t*)(sq + row * 128 + ((q_ch ^ (row & 7)) << 4));
-            rr[k] = *(const u32x4_t*)(rsrc + row * 128 + q_ch * 16);
-          }
-          const int n = n0 + Q * 64 + q_ch * 8;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t bk = mb[Q * 4 + k];
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-              const uint32_t x = v[k][w], r = rr[k][w];
-              const float lo = TypeOps<E>::to_f(lo16<E>(x)) + TypeOps<E>::to_f(lo16<E>(r));
-              const float hi = TypeOps<E>::to_f(hi16<E>(x)) + TypeOps<E>::to_f(hi16<E>(r));
-              const uint32_t b = bk >> (2 * w);
-              v[k][w] = pack2<E>(lo, hi) & (((b & 1u) ? 0x0000ffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u));
-            }
-            const long m = m0 + k * 64 + q_row;
-            if (m < M && n < a.Co) __builtin_nontemporal_store(v[k], (u32x4_t*)(Y + (size_t)m * a.ldy + n));
-          }
-          PP_TS(dbg_it, 5 + 2 * Q);
-          if (Q < 3) {   // the next quarter overwrites the staging area
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            pp_barrier();
-          }
+          tile_of(tile_n, mt_n, nt_n);
+          const long m0n = (long)mt_n * BM;
+          const int n0n = nt_n * BN;
+          if (omask) load_mask(m0n, n0n, mb);   // (the current tile's bits are in mp)
+          setup_lanes(m0n, n0n);
+          par = (nk + par) & 1;
+          prologue();
         }
-        goto rq_done;
       }
+      goto rq_done;
     }
     const E* R1 = (const E*)a.r;
     const E* R2 = (const E*)a.r2;
@@ -802,9 +842,8 @@ int pp_grid(int nwg) {
 
 template <typename E, int ST, int PERSIST>
 hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
-  // two K-tile buffers (the epilogue stages through buffer 1); the one-tile dense 1x1 launches
-  // also the 32 KB quarter staging of the residual epilogue (RQ)
-  constexpr int LDS = PP_LDS + (PERSIST == 2 ? 32768 : 0);
+  // two K-tile buffers (the epilogue stages through buffer 1; RQP: the residual tile)
+  constexpr int LDS = PP_LDS;
   auto kern = conv_nt_pp_kernel<E, ST, PERSIST>;
   static bool attr = false;
   if (!attr) {
@@ -814,18 +853,15 @@ hipError_t pp_launch(const ConvArgs& a, hipStream_t s) {
   }
   const long M = (long)a.N * a.Ho * a.Wo;
   const int nwg = ceil_div(M, 256) * ceil_div(a.Co, 256);
-  hipLaunchKernelGGL(kern, dim3(PERSIST == 1 ? pp_grid(nwg) : nwg), dim3(PP_THREADS), LDS, s, a);
+  hipLaunchKernelGGL(kern, dim3(PERSIST == 1 || PERSIST == 3 ? pp_grid(nwg) : nwg), dim3(PP_THREADS), LDS, s, a);
   return hipGetLastError();
 }
 
-#ifndef PP_RQ
-#define PP_RQ 1   // 0: the RQ launches take the one-tile epilogue's global residual loads (A/B)
-#endif
-
 template <typename E, int ST>
 hipError_t pp_launch_st(const ConvArgs& a, hipStream_t s) {
-  if constexpr (ST == 0 && PP_RQ) {
-    if (a.r && !a.r2 && (long)a.N * a.Ho * a.Wo * a.ldr * 2 < (1L << 31)) return pp_launch<E, 0, 2>(a, s);
+  if constexpr (ST == 0) {   // dense 1 x 1 rows, one residual: the residual tile by LDS-DMA
+    if (a.r && !a.r2 && (long)a.N * a.Ho * a.Wo * a.ldr * 2 < (1L << 31))
+      return pp_launch<E, 0, 3>(a, s);
   }
   if (a.r || a.r2 || a.omask) return pp_launch<E, ST, 0>(a, s);
   return pp_launch<E, ST, 1>(a, s);

@@ -155,20 +155,25 @@ def test_conv_dgrad(cuda, dtype, case):
 # the identity units' data-gradient epilogue (seg_op_conv_dgrad_res): N, H, W, Co (= the
 # forward conv's output channels: dy's), Ci (dx's), with residual, with the consumer's ReLU bits
 RES_CASES = [
-    (2, 16, 32, 256, 512, True, True),     # one-tile ping-pong launch: residual + mask (4 x 2 tiles)
+    (2, 16, 32, 256, 512, True, True),     # persistent residual launch (RQP): residual + mask (4 x 2 tiles)
     (2, 16, 32, 256, 512, True, False),    # residual only
     (1, 20, 20, 128, 256, True, True),     # ragged rows (400 pixels), K 128
     (1, 16, 16, 64, 256, False, True),     # mask only (the premasked dgrad without residual), K 64
     (2, 8, 16, 512, 2048, True, True),     # the block4 shape class: K 512 -> N 2048
     (1, 12, 20, 256, 128, True, False),    # Ci <= 128: the v2 kernel's residual epilogue
+    # RQP with more tiles than CUs (506 tiles: blocks run two, the next tile's mask bytes and
+    # K-tile 0 issued inside the epilogue), a ragged last row tile; K 192 = 3 K-tiles (odd: the
+    # starting buffer alternates tile to tile) and K 256 (even)
+    (4, 63, 257, 192, 512, True, True),
+    (4, 63, 257, 256, 512, True, True),
 ]
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", RES_CASES)
 def test_conv_dgrad_residual_masked(cuda, dtype, case):
-    """dx = round(round(dgrad(dy)) + r), stored with the outputs whose ReLU bit is 0 set to
-    zero (pre-masked identity-unit gradients, staged residuals -- the identity units'
+    """dx = round(dgrad(dy) + r) (RQP: one rounding; the v2 kernel's epilogue rounds the data
+    gradient first), stored with the outputs whose ReLU bit is 0 set to zero (pre-masked identity-unit gradients, staged residuals -- the identity units'
     conv1 data gradient), against a float64 restatement on the same 16-bit operands: kept
     elements at the 16-bit bound of the other op tests (L2-relative), masked-off elements exactly
     zero, the residual read in place (r aliasing dx) bitwise the same as from another buffer."""
@@ -179,11 +184,11 @@ def test_conv_dgrad_residual_masked(cuda, dtype, case):
     w = _round((g.standard_normal((Co, Ci)) * np.sqrt(2.0 / Ci)).astype(np.float32), dtype)
     res = _round(g.standard_normal((N, H, W, Ci)).astype(np.float32), dtype) if with_r else None
     bits = g.integers(0, 256, size=(N, H, W, Ci // 8), dtype=np.uint8) if with_m else None
-    dg = np.einsum("nhwo,oi->nhwi", dy.astype(np.float64), w.astype(np.float64))
+    dg = (dy.reshape(-1, Co).astype(np.float64) @ w.astype(np.float64)).reshape(N, H, W, Ci)
     tdt = TDT[dtype]
     ref = dg
-    if with_r:   # the kernel rounds the data gradient to 16 bits, then adds the residual
-        ref = torch.as_tensor(dg).to(tdt).double().numpy() + res
+    if with_r:   # the exact sum: one rounding (RQP) and two (v2) are both within the bound
+        ref = dg + res
     keep = np.ones((N, H, W, Ci), bool)
     if with_m:
         keep = ((bits[..., :, None] >> np.arange(8)) & 1).astype(bool).reshape(N, H, W, Ci)

@@ -18,11 +18,11 @@ ph = {"main": [], "stats": [], "epi": [], "gap": []}
 # the epilogue's pieces (stamps 4-11): per column half the staging writes (from the previous
 # stamp), statistics, staging barrier, staging reads + stores
 sub = {f"q{q}_{n}": [] for q in (0, 1) for n in ("stage", "stats", "bar", "store")}
-# RQ=1 (the one-tile residual epilogue, four 64-column quarters): stamps 4 + 2Q after the
-# quarter's staging writes, residual wait and barrier, 5 + 2Q after its stores
+# RQ=1 (the one-tile residual epilogue, in place per 128-column half): stamps 4 + 3h after the
+# residual wait and barrier, 5 + 3h after the in-place sums and barrier, 6 + 3h after the stores
 RQ = os.environ.get("RQ") == "1"
 if RQ:
-    sub = {f"Q{q}_{n}": [] for q in range(4) for n in ("stage_wait", "store")}
+    sub = {f"h{q}_{n}": [] for q in range(2) for n in ("wait", "add", "store")}
 for b in range(256):
     for i in range(n[b]):
         r = t[b, i]
@@ -31,10 +31,10 @@ for b in range(256):
             ph["gap"].append(t[b, i + 1, 0] - r[3])
         if r[4] > 0 and RQ:
             prev = r[2]
-            for q in range(4):
-                for j, nm in enumerate(("stage_wait", "store")):
-                    sub[f"Q{q}_{nm}"].append(r[4 + 2 * q + j] - prev)
-                    prev = r[4 + 2 * q + j]
+            for q in range(2):
+                for j, nm in enumerate(("wait", "add", "store")):
+                    sub[f"h{q}_{nm}"].append(r[4 + 3 * q + j] - prev)
+                    prev = r[4 + 3 * q + j]
         elif r[4] > 0:
             prev = r[2]
             for q in (0, 1):
