@@ -166,6 +166,8 @@ RES_CASES = [
     # starting buffer alternates tile to tile) and K 256 (even)
     (4, 63, 257, 192, 512, True, True),
     (4, 63, 257, 256, 512, True, True),
+    # the consumer's ReLU bits without a residual (one-tile launches), 506 tiles, ragged, K 192
+    (4, 63, 257, 192, 512, False, True),
 ]
 
 
