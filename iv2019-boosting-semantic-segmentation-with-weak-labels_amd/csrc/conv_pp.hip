@@ -24,14 +24,18 @@
 //    offset per lane, padding taps and rows past the tensor given an out-of-range offset so
 //    the buffer unit writes zeros (4 VALU per A DMA, 1 per B DMA: the load segment is short);
 //  * K-tiles run channel-chunk-major, tap-minor, so the KH*KW shifted reads of one chunk's
-//    source rows hit L2 (dilated 3x3: +6 %).
+//    source rows hit L2 (dilated 3x3: +6 %);
+//  * persistent over tiles (the next tile's K-tile 0 in flight during the epilogue); the data
+//    gradients with one residual (dense 1 x 1 rows) take the residual tile by LDS-DMA and add it
+//    in place (RQP, PERSIST = 3); two residuals or other shapes run one tile per workgroup.
 #include "conv.h"
 #include <cstdlib>
 
 #ifdef PP_DBG_TIMING
 // A/B only: per-block, per-tile timestamps (s_memtime) of the NT persistent loop
 // (stamps 0-3: tile start, main loop done, prologue issued, epilogue done; 4-11: per column half
-// qn the staging writes, statistics, staging barrier and stores, at 4 + 4 qn + 0..3)
+// qn the staging writes, statistics, staging barrier and stores, at 4 + 4 qn + 0..3; RQP: per
+// half the residual wait, in-place sums + barrier and stores at 4 + 3 qn + 0..2)
 __device__ unsigned long long g_pp_dbg[256 * 16 * 16];
 #define PP_TS(it, k) \
   if (threadIdx.x == 0 && blockIdx.x < 256 && (it) < 16) g_pp_dbg[(blockIdx.x * 16 + (it)) * 16 + (k)] = __builtin_amdgcn_s_memtime()
