@@ -272,9 +272,10 @@ int seg_op_conv_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Co, 
                       int H, int W, void* dx, int lddx, void* stream);
 /* a 1 x 1 stride-1 data gradient with the identity units' epilogue: dx = dgrad(dy) + r (r may
  * be NULL; it may alias dx), stored masked by omask (ReLU bits [M][Ci/8], bit e of byte n/8 =
- * channel n; NULL = unmasked) -- the one-tile launches of the pre-masked residual chain
- * (pre-masked identity-unit gradients, staged residuals); 16-bit dtypes take the
- * ping-pong kernel for Ci > 128 */
+ * channel n; NULL = unmasked) -- the launches of the pre-masked residual chain (DESIGN.md §5b'',
+ * §5f); 16-bit dtypes take the ping-pong kernel for Ci > 128: with r, persistent with the
+ * residual tile by LDS-DMA and one rounding of dgrad + r (RQP); without, one tile per
+ * workgroup */
 int seg_op_conv_dgrad_res(int dtype, const void* dy, int N, int H, int W, int Co, int lddy,
                           const void* wt, int Ci, void* dx, int lddx, const void* r, int ldr,
                           const uint8_t* omask, void* stream);
