@@ -427,7 +427,7 @@ def main():
         # HBM bytes per launch of that class from the committed PMC passes of this code
         # (tools/pmc_traffic.sh + tools/pmc_traffic.py; rocprofv3 cannot run inside the bench)
         traffic, tsrc, step_ledger = None, None, None
-        for tname in ("r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json",
+        for tname in ("r06_s25_pmc_traffic.json", "r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json",
                       "r01_pmc_traffic.json"):
             tpath = os.path.join(REPO, "profiles", tname)
             if not os.path.exists(tpath):
