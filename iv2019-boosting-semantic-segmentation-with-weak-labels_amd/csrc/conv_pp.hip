@@ -365,7 +365,9 @@ __device__ __forceinline__ void conv_nt_pp_body(const ConvArgs& a) {
   auto issue_resw = [&](int hh, char* dst) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const uint32_t sb = (uint32_t)((((int)m0 + wm * 128 + i * 16) * a.ldr + n0 + hh * 128 + wn * 32) * 2);
+      // (unsigned: rows past M may wrap; they are read, never stored)
+      const uint32_t sb = ((uint32_t)m0 + (uint32_t)(wm * 128 + i * 16)) * (uint32_t)a.ldr * 2u +
+                          (uint32_t)(n0 + hh * 128 + wn * 32) * 2u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs_r, (__attribute__((address_space(3))) void*)(dst + wn * 16384 + (wm * 128 + i * 16) * 64), 16, rw_lane + sb, 0, 0, 0);
     }
