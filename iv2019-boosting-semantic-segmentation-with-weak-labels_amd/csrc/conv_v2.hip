@@ -1210,14 +1210,21 @@ bool conv_wgrad_v2_ok(const WgradArgs& a) {
 
 // tile (BM co x BN cols): the largest the extents fill -- 256 x 256 (wave tiles 128 x 64)
 // keeps LDS fragment traffic below the MFMA time and halves L2 re-reads vs 128 x 256 -- then
-// halved (larger side first) while tiles x pixel splits would leave CUs idle (small outputs
-// such as 256 x 256 1x1 convs: 1 tile x 64 splits = 64 workgroups otherwise)
+// halved (larger side first) while tiles x pixel splits would leave fewer than 128 workgroups
+// (small outputs such as 256 x 256 1x1 convs: 1 tile x 64 splits = 64 workgroups otherwise).
+// 128, the side stream's workgroup target (wgrad_splits): halving down to 256 workgroups
+// (round 5) gave block2 / head 1 x 1 layers 128 x 128 tiles where 128 x 256 / 256 x 128 now
+// run at the same workgroup count with half the operand re-reads: step +0.53 % (three
+// interleaved pairs, profiles/r06_s30_wgrad_tile_target.txt; 64: +0.27 %)
 void conv_wgrad_v2_tile(int Co, int Ncol, long P, int* bm, int* bn) {
   int m = Co <= 64 ? 64 : (Co <= 128 ? 128 : 256);
   int n = Ncol <= 64 ? 64 : (Ncol <= 128 ? 128 : 256);
   const long maxs = std::min<long>(256, std::max<long>(1, P / 2048));
   auto blocks = [&]() { return (long)((Co + m - 1) / m) * ((Ncol + n - 1) / n) * maxs; };
-  while (blocks() < 256) {
+#ifndef WG_TILE_TARGET
+#define WG_TILE_TARGET 128
+#endif
+  while (blocks() < WG_TILE_TARGET) {
     if (m >= n && m > 64) m /= 2;
     else if (n > 64) n /= 2;
     else break;
