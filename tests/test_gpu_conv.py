@@ -166,6 +166,11 @@ RES_CASES = [
     # starting buffer alternates tile to tile) and K 256 (even)
     (4, 63, 257, 192, 512, True, True),
     (4, 63, 257, 256, 512, True, True),
+    # ragged columns: Ci = 384 / 320 leave the last column tile half / three-quarters empty
+    # (RQP reads past the row end into the next row or past the buffer, never stores there),
+    # with ragged rows (640 pixels) and 3 K-tiles
+    (2, 16, 32, 256, 384, True, True),
+    (1, 16, 40, 192, 320, True, True),
     # the consumer's ReLU bits without a residual (one-tile launches), 506 tiles, ragged, K 192
     (4, 63, 257, 192, 512, False, True),
 ]
